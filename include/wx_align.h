@@ -1,0 +1,116 @@
+/*
+ * wx_align.h — C ABI of the MI355X (gfx950) forced-alignment + VAD-segmentation library
+ * (libwxalign.so, built from whisperx_amd/csrc/wx_align.hip).
+ *
+ * The reference (NADOOIT/whisperX @ 2025-01-12) is pure Python; these entry points replace
+ * the CPU functions on its alignment / VAD hot path, batched over many segments:
+ *
+ *   wx_trellis        <- whisperx/alignment.py:359  get_trellis(emission, tokens, blank_id)
+ *   wx_backtrack      <- whisperx/alignment.py:387  backtrack(trellis, emission, tokens, blank_id)
+ *   wx_merge_repeats  <- whisperx/alignment.py:438  merge_repeats(path, transcript)
+ *   wx_align_dp       <- whisperx/alignment.py:242-250 (get_trellis -> backtrack ->
+ *                        merge_repeats as align() chains them), fused: the trellis is never
+ *                        materialised; a 1-bit decision map replaces it for the backtrack.
+ *   wx_binarize       <- whisperx/vad.py:118  Binarize.__call__ (hysteresis + min-cut),
+ *                        the kernel under vad.py:264 merge_chunks
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers (allocated by the caller; the library never
+ *     allocates).  Sizes passed by value are host integers.  `stream` is a hipStream_t
+ *     (NULL = default stream); every call only enqueues work on it.
+ *   - Segments are CSR-packed.  Segment s has T_s = em_off[s+1]-em_off[s] emission rows
+ *     starting at row em_off[s] of `em` ([sum_T, V] fp32 row-major log-probabilities) and
+ *     N_s = tok_off[s+1]-tok_off[s] token ids starting at tok[tok_off[s]].
+ *   - Return 0 on success or a WX_E_* / hipError_t code; wx_strerror() names it.
+ *     A per-segment alignment failure (the reference's backtrack() returning None) is data
+ *     (status / path_len = -1), never an error code.
+ *   - Reentrant; no global mutable state; one device per call (the current device).
+ *   - Semantics follow the reference's torch-CPU arithmetic bit-for-bit (fp32 adds,
+ *     NaN-propagating max, strict `>` backtrack test, fp64-accumulated column-0 cumsum),
+ *     except path probabilities, which use the correctly rounded fp32 exp (the reference's
+ *     MKL exp differs from it by at most 1 ULP).
+ */
+#ifndef WX_ALIGN_H
+#define WX_ALIGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    WX_OK = 0,
+    WX_E_INVALID = 1001,   /* bad argument (null pointer, negative size, blank out of range) */
+    WX_E_VOCAB = 1002,     /* V outside [1, WX_MAX_VOCAB] */
+    WX_E_TOO_LONG = 1003,  /* a segment has more tokens than WX_MAX_TOKENS */
+    WX_E_WORKSPACE = 1004, /* workspace too small (see the *_workspace_bytes queries) */
+    WX_E_LAUNCH = 1005     /* kernel launch failed */
+};
+
+#define WX_MAX_VOCAB 64      /* emission columns held in LDS per row */
+#define WX_MAX_TOKENS 2048   /* tokens per segment (64 lanes x 32 cells) */
+
+const char* wx_version(void);
+const char* wx_strerror(int code);
+
+/* get_trellis (alignment.py:359-379), batched.  trellis is CSR: segment s occupies
+ * (T_s+1)*(N_s+1) floats starting at element tr_off[s] (row-major [T_s+1][N_s+1]).
+ * max_N = max_s N_s (host). */
+int wx_trellis(const float* em, const int64_t* em_off, int32_t V,
+               const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
+               int32_t S, int64_t max_N, float* trellis, const int64_t* tr_off, void* stream);
+
+/* backtrack (alignment.py:387-421) from a materialised trellis, batched.  The path of
+ * segment s is written in forward (time-increasing) order at element em_off[s] of
+ * path_tok/path_time/path_prob (capacity T_s); path_len[s] = its length or -1 (None);
+ * t_start[s] = argmax of the trellis' last column (first max, NaN counted as max). */
+size_t wx_backtrack_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
+int wx_backtrack(const float* trellis, const int64_t* tr_off,
+                 const float* em, const int64_t* em_off, int32_t V,
+                 const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
+                 int32_t S, int64_t max_N, int64_t sum_T,
+                 int32_t* path_tok, int32_t* path_time, float* path_prob,
+                 int32_t* path_len, int32_t* t_start,
+                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* merge_repeats (alignment.py:438-454), batched over paths stored at path_off[s] with
+ * length path_len[s] (<0 = no path -> seg_count 0).  Segments are written at the same
+ * offsets (capacity = path length): token index, start frame, end frame (exclusive), mean
+ * probability (left-to-right fp64 sum / count, as Python's sum()). */
+int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const float* path_prob,
+                     const int64_t* path_off, const int32_t* path_len, int32_t S,
+                     int32_t* seg_tok, int32_t* seg_start, int32_t* seg_end, double* seg_score,
+                     int32_t* seg_count, void* stream);
+
+/* The fused align() DP.  For every segment: trellis recurrence with a 1-bit decision map
+ * (never materialised), argmax, backtrack and merge_repeats.  Outputs are CSR by tok_off:
+ * seg_start/seg_end (frames, end exclusive) and seg_score of token k (the k-th
+ * merge_repeats segment; a successful path always yields exactly N_s of them).
+ * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None).
+ * min_N/max_N/sum_T describe the batch (host values). */
+size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
+int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
+                const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
+                int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T,
+                int32_t* seg_start, int32_t* seg_end, double* seg_score,
+                int32_t* t_start, int32_t* status,
+                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Binarize.__call__ (vad.py:118-180) for n_files score columns (CSR by f_off) with
+ * pyannote sliding-window geometry per file (frame i is centred at
+ * 0.5*(s + (s + duration)), s = start + i*step).  onset/offset compared in fp32.
+ * Regions [reg_start, reg_end] (seconds) of file f are written at reg_off[f] (capacity
+ * reg_off[f+1]-reg_off[f]; F_f+1 always suffices); reg_count[f] = count, or -1 on
+ * overflow.  Regions of length <= 1e-6 s are dropped (pyannote Annotation semantics). */
+int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files,
+                const double* sw_start, const double* sw_step, const double* sw_duration,
+                float onset, float offset, double max_duration, double pad_onset, double pad_offset,
+                double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WX_ALIGN_H */

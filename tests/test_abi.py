@@ -1,0 +1,80 @@
+"""The C-ABI library loads and exports every symbol include/wx_align.h declares (CPU only:
+no compute calls; argument validation paths return before any launch)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "wx_align.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(wx_[a-z_0-9]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from whisperx_amd import _lib
+
+    _lib.build()
+    return _lib.load(require_device=False)
+
+
+def test_header_lists_expected_entry_points():
+    syms = declared_symbols()
+    for s in ("wx_align_dp", "wx_trellis", "wx_backtrack", "wx_merge_repeats", "wx_binarize"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from whisperx_amd import _lib
+
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} not bound in _lib.SIGNATURES"
+
+
+def test_version_and_errors(lib):
+    assert b"gfx950" in lib.wx_version()
+    assert lib.wx_strerror(0) == b"ok"
+    assert b"workspace" in lib.wx_strerror(1004)
+
+
+def test_workspace_queries_monotone(lib):
+    a = lib.wx_align_dp_workspace_bytes(64, 64 * 1499, 500)
+    b = lib.wx_align_dp_workspace_bytes(128, 128 * 1499, 500)
+    assert 0 < a < b
+    assert lib.wx_backtrack_workspace_bytes(4, 4000, 900) > 0
+
+
+def test_argument_validation_without_device(lib):
+    # S < 0 and oversized vocab/tokens are rejected before anything touches the device
+    assert lib.wx_align_dp(None, None, 32, None, None, None, -1, 0, 0, 0, None, None, None, None, None,
+                           None, 0, None) == 1001
+    assert lib.wx_align_dp(None, None, 32, None, None, None, 0, 0, 0, 0, None, None, None, None, None,
+                           None, 0, None) == 0
+    dummy = ctypes.c_void_p(8)
+    assert lib.wx_align_dp(dummy, dummy, 100, dummy, dummy, dummy, 1, 1, 1, 10, dummy, dummy, dummy, dummy,
+                           dummy, dummy, 1 << 30, None) == 1002
+    assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 5000, 10, dummy, dummy, dummy, dummy,
+                           dummy, dummy, 1 << 30, None) == 1003
+    assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 10, 10, dummy, dummy, dummy, dummy,
+                           dummy, dummy, 16, None) == 1004
+    assert lib.wx_binarize(None, None, -1, None, None, None, 0.5, 0.3, 1.0, 0.0, 0.0, None, None, None, None,
+                           None) == 1001
+
+
+def test_product_refuses_without_device():
+    import torch
+
+    from whisperx_amd import _lib
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible")
+    with pytest.raises(_lib.WXError):
+        _lib.load(require_device=True)

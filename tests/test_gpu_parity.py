@@ -1,0 +1,302 @@
+"""HIP path (through the C ABI) against the reference's golden vectors and the CPU oracle.
+
+Tolerances: token paths, t_start, frame spans, timestamps and trellis values are bit-exact.
+Path probabilities: <= 1 fp32 ULP from the reference (its torch-CPU exp is MKL's; the GPU
+uses the correctly rounded exp, as the oracle does, so GPU == oracle bit for bit);
+merge_repeats scores: relative 2.5e-7 from the reference, == oracle (fp64, 1e-15 rel)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from align_helpers import compare, jsonable, run_scenario, scenarios
+from conftest import GOLDEN, ulp_diff
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from whisperx_amd import _lib
+
+    _lib.load()
+
+
+def _batch(cases):
+    from whisperx_amd import _lib
+
+    ems = [torch.from_numpy(c["em"]).to(DEV) for c in cases]
+    toks = [c["tokens"].tolist() for c in cases]
+    blanks = [int(c["blank"]) for c in cases]
+    return _lib.Batch(ems, toks, blanks, device=DEV)
+
+
+def _by_vocab(dp_cases):
+    groups = {}
+    for i in range(len(dp_cases)):
+        c = dp_cases[i]
+        groups.setdefault(c["em"].shape[1], []).append((i, c))
+    return groups
+
+
+# --------------------------------------------------------------------- fused align DP
+def test_align_dp_matches_reference_golden(dp_cases):
+    from whisperx_amd import _lib
+
+    for V, items in _by_vocab(dp_cases).items():
+        cases = [c for _, c in items]
+        b = _batch(cases)
+        ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b))
+        for s, (i, c) in enumerate(items):
+            assert ts[s] == int(c["t_start"]), f"case {i}: t_start {ts[s]} != {int(c['t_start'])}"
+            ok = int(c["path_ok"]) == 1
+            assert (st[s] == 0) == ok, f"case {i}: status {st[s]}"
+            if not ok:
+                continue
+            a, e = b.tok_off[s], b.tok_off[s + 1]
+            assert np.array_equal(ss[a:e], c["seg_start"]), f"case {i}: seg_start"
+            assert np.array_equal(se[a:e], c["seg_end"]), f"case {i}: seg_end"
+            assert np.allclose(sc[a:e], c["seg_score"], rtol=2.5e-7, atol=0, equal_nan=True), f"case {i}"
+            okc, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
+            assert np.array_equal(sc[a:e], sco, equal_nan=True) or np.allclose(sc[a:e], sco, rtol=1e-15,
+                                                                               equal_nan=True), f"case {i}"
+
+
+def _random_cases(rng, n, T_range, N_range, V, quant=None, blank=None):
+    cases = []
+    for _ in range(n):
+        T = int(rng.integers(*T_range))
+        N = int(rng.integers(*N_range))
+        bl = int(rng.integers(0, V)) if blank is None else blank
+        logits = rng.standard_normal((T, V)).astype(np.float32)
+        logits[:, bl] += 6.0
+        nb = np.array([v for v in range(V) if v != bl])
+        toks = nb[rng.integers(0, len(nb), N)]
+        if N <= T - 2:
+            fr = np.sort(rng.choice(np.arange(1, T - 1), N, replace=False))
+            logits[fr, toks] += 12.0
+        em = torch.log_softmax(torch.from_numpy(logits), -1).numpy()
+        if quant:
+            em = (np.round(em * quant) / quant).astype(np.float32)
+        cases.append({"em": np.ascontiguousarray(em), "tokens": toks.astype(np.int64), "blank": np.int64(bl)})
+    return cases
+
+
+def _check_vs_oracle(cases, tag):
+    from whisperx_amd import _lib
+
+    b = _batch(cases)
+    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b))
+    mism = 0
+    for s, c in enumerate(cases):
+        ok, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
+        assert ts[s] == tso, f"{tag} seg {s}: t_start {ts[s]} vs {tso}"
+        assert (st[s] == 0) == ok, f"{tag} seg {s}: status"
+        if ok:
+            a, e = b.tok_off[s], b.tok_off[s + 1]
+            assert np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo), f"{tag} seg {s}: spans"
+            mism += int((sc[a:e] != sco).sum())
+            assert np.allclose(sc[a:e], sco, rtol=1e-12, atol=0, equal_nan=True), f"{tag} seg {s}: scores"
+    return mism
+
+
+@pytest.mark.parametrize("V", [29, 32, 40, 64])
+def test_align_dp_random_mixed_buckets_vs_oracle(V):
+    rng = np.random.default_rng(V)
+    cases = []
+    # every cells-per-lane bucket: N in (1..64], (64..128], ... (1536..2048]
+    for lo, hi in [(1, 65), (65, 129), (129, 257), (257, 385), (385, 513), (513, 769), (769, 1025),
+                   (1025, 1537), (1537, 2049)]:
+        cases += _random_cases(rng, 2, (max(hi + 8, 40), hi + 700), (lo, hi), V)
+    cases += _random_cases(rng, 6, (20, 300), (1, 60), V, quant=16)  # exact ties
+    cases += _random_cases(rng, 4, (5, 40), (20, 60), V)  # N > T: backtrack fails
+    _check_vs_oracle(cases, f"V{V}")
+
+
+def test_align_dp_config2_batch_vs_oracle():
+    """BASELINE config 2: 64 x 30 s segments (T=1499, V=32, N~U[300,500])."""
+    rng = np.random.default_rng(2)
+    cases = _random_cases(rng, 64, (1499, 1500), (300, 501), 32, blank=0)
+    _check_vs_oracle(cases, "cfg2")
+
+
+def test_align_dp_config5_long_form_vs_oracle():
+    """BASELINE config 5: DE large-xlsr-shaped, T=2999, V=40, N~900."""
+    rng = np.random.default_rng(5)
+    cases = _random_cases(rng, 8, (2999, 3000), (850, 951), 40, blank=0)
+    _check_vs_oracle(cases, "cfg5")
+
+
+def test_align_dp_deterministic_and_order_independent():
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(11)
+    cases = _random_cases(rng, 12, (100, 900), (20, 300), 32)
+    r1 = [x.cpu().numpy() for x in _lib.align_dp(_batch(cases))]
+    r2 = [x.cpu().numpy() for x in _lib.align_dp(_batch(cases))]
+    for a, b in zip(r1, r2):
+        assert np.array_equal(a, b, equal_nan=True)
+    # a segment's result does not depend on its batch neighbours
+    single = [x.cpu().numpy() for x in _lib.align_dp(_batch(cases[5:6]))]
+    b = _batch(cases)
+    a0, a1 = b.tok_off[5], b.tok_off[6]
+    assert np.array_equal(r1[0][a0:a1], single[0][: a1 - a0])
+    assert np.array_equal(r1[2][a0:a1], single[2][: a1 - a0])
+
+
+# --------------------------------------------------------------- get_trellis / backtrack
+def test_trellis_matches_reference_golden(dp_cases):
+    from whisperx_amd import _lib
+
+    for V, items in _by_vocab(dp_cases).items():
+        b = _batch([c for _, c in items])
+        flat, offs = _lib.trellis(b)
+        flat = flat.cpu().numpy()
+        for s, (i, c) in enumerate(items):
+            T, N = c["em"].shape[0], len(c["tokens"])
+            tr = flat[offs[s]:offs[s + 1]].reshape(T + 1, N + 1)
+            if "trellis" in c:
+                assert np.array_equal(tr, c["trellis"], equal_nan=True), f"case {i}"
+            if not np.isnan(tr).any():
+                assert hashlib.sha256(tr.tobytes()).digest() == c["trellis_sha"].tobytes(), f"case {i}"
+            assert np.array_equal(tr[:, -1], c["trellis_colN"], equal_nan=True), f"case {i}"
+
+
+def test_backtrack_matches_reference_golden(dp_cases):
+    from whisperx_amd import _lib
+
+    for V, items in _by_vocab(dp_cases).items():
+        b = _batch([c for _, c in items])
+        flat, offs = _lib.trellis(b)
+        pt, pm, pp, plen, ts = (x.cpu().numpy() for x in _lib.backtrack(b, flat, offs))
+        for s, (i, c) in enumerate(items):
+            assert ts[s] == int(c["t_start"]), f"case {i}"
+            if not int(c["path_ok"]):
+                assert plen[s] == -1, f"case {i}"
+                continue
+            L = plen[s]
+            o = b.em_off[s]
+            assert L == len(c["path_tok"]), f"case {i}: len {L}"
+            assert np.array_equal(pt[o:o + L], c["path_tok"]) and np.array_equal(pm[o:o + L], c["path_time"])
+            assert ulp_diff(pp[o:o + L], c["path_prob"].astype(np.float32)).max() <= 1, f"case {i}"
+
+
+def test_merge_repeats_kernel_on_reference_paths(dp_cases):
+    from whisperx_amd import _lib
+
+    paths = [dp_cases[i] for i in range(len(dp_cases)) if int(dp_cases[i]["path_ok"])]
+    off = [0]
+    for c in paths:
+        off.append(off[-1] + len(c["path_tok"]))
+    cat = lambda k, dt: torch.from_numpy(np.concatenate([c[k] for c in paths]).astype(dt)).to(DEV)  # noqa: E731
+    st, ss, se, sc, cnt = _lib.merge_repeats(cat("path_tok", np.int32), cat("path_time", np.int32),
+                                             cat("path_prob", np.float32),
+                                             torch.tensor(off[:-1], dtype=torch.int64).to(DEV),
+                                             torch.tensor([len(c["path_tok"]) for c in paths], dtype=torch.int32).to(DEV),
+                                             DEV)
+    ss, se, sc, cnt = ss.cpu().numpy(), se.cpu().numpy(), sc.cpu().numpy(), cnt.cpu().numpy()
+    for p, c in enumerate(paths):
+        G = cnt[p]
+        o = off[p]
+        assert G == len(c["seg_start"])
+        assert np.array_equal(ss[o:o + G], c["seg_start"]) and np.array_equal(se[o:o + G], c["seg_end"])
+        # probabilities fed as the reference's own fp32 values -> scores bit-exact
+        assert np.array_equal(sc[o:o + G], c["seg_score"], equal_nan=True)
+
+
+def test_python_api_objects(dp_cases):
+    from whisperx_amd import backtrack, get_trellis, merge_repeats, merge_words
+
+    c = dp_cases[26]
+    em = torch.from_numpy(c["em"])
+    toks = c["tokens"].tolist()
+    tr = get_trellis(em, toks, int(c["blank"]))
+    assert tr.device.type == "cpu" and tuple(tr.shape) == (em.shape[0] + 1, len(toks) + 1)
+    assert hashlib.sha256(tr.numpy().tobytes()).digest() == c["trellis_sha"].tobytes()
+    path = backtrack(tr, em, toks, int(c["blank"]))
+    assert [p.token_index for p in path] == c["path_tok"].tolist()
+    assert [p.time_index for p in path] == c["path_time"].tolist()
+    transcript = "".join(chr(97 + (int(x) % 26)) for x in toks)
+    segs = merge_repeats(path, transcript)
+    assert [s.start for s in segs] == c["seg_start"].tolist()
+    assert [s.end for s in segs] == c["seg_end"].tolist()
+    assert [ord(s.label) for s in segs] == c["seg_label"].tolist()
+    words = merge_words(segs, separator=transcript[0])
+    assert [w.start for w in words] == c["word_start"].tolist()
+    assert [w.end for w in words] == c["word_end"].tolist()
+    assert np.allclose([w.score for w in words], c["word_score"], rtol=1e-6)
+    # failure -> None
+    bad = dp_cases[4]
+    em = torch.from_numpy(bad["em"])
+    tr = get_trellis(em, bad["tokens"].tolist(), 0)
+    assert backtrack(tr, em, bad["tokens"].tolist(), 0) is None
+
+
+# ------------------------------------------------------------------------ align() e2e
+@pytest.mark.parametrize("si", range(len(scenarios())))
+def test_align_end_to_end_matches_reference(si, capsys):
+    """Fake CTC model on the GPU: log_softmax runs on the device, the DP in the fused kernel.
+    Timestamps must match the reference to within one frame; in practice they are exact."""
+    from whisperx_amd import align
+
+    sc, logits = scenarios()[si]
+    stats = {}
+    out, mutated = run_scenario(align, sc, logits, DEV)
+    compare(jsonable(out), sc["result"], time_tol=0.02 + 1e-9, score_tol=1e-3 + 1e-9, stats=stats)
+    assert jsonable(mutated) == sc["mutated"]
+    if stats.get("abs_err"):
+        assert float(np.mean(stats["abs_err"])) * 1000 <= 1.0  # word-boundary MAE (ms)
+
+
+# ------------------------------------------------------------------------------ VAD
+def _vad():
+    with open(os.path.join(GOLDEN, "vad_cases.json")) as f:
+        meta = json.load(f)
+    return meta, np.load(os.path.join(GOLDEN, "vad_cases.npz"))
+
+
+def test_binarize_and_merge_chunks_match_reference():
+    from whisperx_amd.vad import Binarize, SlidingWindow, SlidingWindowFeature, merge_chunks
+
+    meta, arr = _vad()
+    for ci, c in enumerate(meta["cases"]):
+        sc = arr[f"v{ci:02d}_scores"]
+        feat = SlidingWindowFeature(sc[:, None], SlidingWindow(c["sw_start"], c["sw_step"], c["sw_duration"]))
+        ann = Binarize(max_duration=c["chunk_size"], onset=c["onset"], offset=c["offset"])(feat)
+        assert [[s.start, s.end] for s in ann.get_timeline()] == c["regions"], f"vad case {ci}"
+        chunks = merge_chunks(feat, c["chunk_size"], onset=c["onset"], offset=c["offset"])
+        got = [{"start": x["start"], "end": x["end"], "segments": [list(p) for p in x["segments"]]} for x in chunks]
+        assert got == c["chunks"], f"vad case {ci}"
+    m = meta["min_duration_on"]
+    sc = arr["vmin_scores"]
+    feat = SlidingWindowFeature(sc[:, None], SlidingWindow(0.0, 0.016875, 0.0619375))
+    ann = Binarize(onset=m["onset"], offset=m["offset"], min_duration_on=m["min_duration_on"])(feat)
+    assert [[s.start, s.end] for s, _ in ann.itertracks()] == m["regions"]
+
+
+def test_binarize_one_hour_vs_oracle():
+    """BASELINE config 3 scale: 1 h of VAD scores (213,333 frames), several chunk sizes."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(3)
+    F = 213_333
+    x = rng.standard_normal(F + 40)
+    y = np.convolve(x, np.ones(40) / 40, mode="valid")[:F] * 4 * np.sqrt(40) / 3
+    sc = (1 / (1 + np.exp(-y))).astype(np.float32)
+    for chunk in (30, 10, 2.5):
+        regs = oracle.binarize(sc, 0.0, 0.016875, 0.0619375, 0.5, 0.363, max_duration=chunk)
+        (rs, re), = _lib.binarize([sc], [(0.0, 0.016875, 0.0619375)], 0.5, 0.363, chunk)
+        assert list(zip(rs.tolist(), re.tolist())) == regs, f"chunk {chunk}"
+    # many files in one launch
+    cols = [sc[i * 20000:(i + 1) * 20000 + i * 7] for i in range(8)]
+    outs = _lib.binarize(cols, [(0.25 * i, 0.016875, 0.0619375) for i in range(8)], 0.5, 0.363, 30)
+    for i, (rs, re) in enumerate(outs):
+        assert list(zip(rs.tolist(), re.tolist())) == oracle.binarize(cols[i], 0.25 * i, 0.016875, 0.0619375,
+                                                                       0.5, 0.363, max_duration=30)

@@ -1,0 +1,279 @@
+"""ctypes binding of libwxalign.so (C ABI in include/wx_align.h).
+
+The library is the only compute path of this package: there is no CPU fallback.  If the
+shared object is missing, or no HIP device is visible, every entry point raises.
+
+Tensors are PyTorch device tensors (torch is plumbing here: device memory and streams);
+the library sees raw device pointers, sizes and the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwxalign.so")
+SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+
+MAX_VOCAB = 64
+MAX_TOKENS = 2048
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol declared in include/wx_align.h
+SIGNATURES = {
+    "wx_version": (ctypes.c_char_p, []),
+    "wx_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "wx_trellis": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp]),
+    "wx_backtrack_workspace_bytes": (_sz, [_i32, _i64, _i64]),
+    "wx_backtrack": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64,
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "wx_merge_repeats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "wx_align_dp_workspace_bytes": (_sz, [_i32, _i64, _i64]),
+    "wx_align_dp": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
+                                   _vp, _vp, _vp, _vp, _vp]),
+}
+
+
+class WXError(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/wx_align.hip for gfx950 into libwxalign.so (in-tree)."""
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= _newest_source():
+        return LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", f"-I{INCLUDE_DIR}", "-o", LIB_PATH + ".tmp", SRC_PATH]
+    res = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if res.returncode != 0:
+        raise WXError(f"hipcc failed ({res.returncode}):\n{res.stderr}")
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def _newest_source() -> float:
+    paths = [SRC_PATH, os.path.join(INCLUDE_DIR, "wx_align.h")]
+    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(require_device: bool = True) -> ctypes.CDLL:
+    """Load the HIP library.  Raises if it was not built or (by default) no GPU is visible."""
+    global _lib
+    if require_device and not torch.cuda.is_available():
+        raise WXError("whisperx_amd needs a HIP device (MI355X); none is visible and there is no CPU fallback")
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise WXError(f"{LIB_PATH} is missing: run whisperx_amd._lib.build() (hipcc, gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise WXError(f"libwxalign error {rc}: {load(False).wx_strerror(rc).decode()}")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dev_i64(x, device):
+    return torch.as_tensor(x, dtype=torch.int64).to(device, non_blocking=True)
+
+
+class Workspace:
+    """Grow-only device scratch buffer (avoids an allocation per call)."""
+
+    def __init__(self):
+        self.buf: dict = {}
+
+    def get(self, device, nbytes: int) -> torch.Tensor:
+        key = str(device)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_ws = Workspace()
+
+
+# ----------------------------------------------------------------------------------- batch
+class Batch:
+    """CSR packing of S segments: emissions [sum_T, V] fp32, tokens int32, blank ids."""
+
+    def __init__(self, emissions, tokens, blank_ids, device=None):
+        if len(emissions) != len(tokens) or len(tokens) != len(blank_ids):
+            raise ValueError("emissions, tokens and blank_ids must have the same length")
+        self.S = len(emissions)
+        device = torch.device(device) if device is not None else (
+            emissions[0].device if self.S and emissions[0].is_cuda else torch.device("cuda", torch.cuda.current_device()))
+        self.device = device
+        Ts = [int(e.shape[0]) for e in emissions]
+        Vs = {int(e.shape[1]) for e in emissions if e.dim() == 2}
+        if len(Vs) > 1:
+            raise ValueError("all emissions of a batch must have the same vocabulary size")
+        self.V = Vs.pop() if Vs else 1
+        self.Ns = [len(t) for t in tokens]
+        self.Ts = Ts
+        self.em_off = [0]
+        for T in Ts:
+            self.em_off.append(self.em_off[-1] + T)
+        self.tok_off = [0]
+        for N in self.Ns:
+            self.tok_off.append(self.tok_off[-1] + N)
+        self.sum_T = self.em_off[-1]
+        if self.S:
+            em = torch.cat([e.to(device=device, dtype=torch.float32).reshape(-1, self.V) for e in emissions], 0)
+        else:
+            em = torch.empty((0, self.V), dtype=torch.float32, device=device)
+        self.em = em.contiguous()
+        flat = [int(x) for t in tokens for x in t]
+        self.tok = torch.tensor(flat if flat else [0], dtype=torch.int32).to(device, non_blocking=True)
+        self.blank = torch.tensor([int(b) for b in blank_ids] or [0], dtype=torch.int32).to(device, non_blocking=True)
+        self.em_off_d = _dev_i64(self.em_off, device)
+        self.tok_off_d = _dev_i64(self.tok_off, device)
+        self.min_N = min(self.Ns) if self.Ns else 0
+        self.max_N = max(self.Ns) if self.Ns else 0
+
+
+def _validate(b: Batch):
+    if b.V < 1 or b.V > MAX_VOCAB:
+        raise WXError(f"vocabulary size {b.V} outside [1, {MAX_VOCAB}] (compact the emission columns first)")
+    if b.max_N > MAX_TOKENS:
+        raise WXError(f"a segment has {b.max_N} tokens; the kernel supports up to {MAX_TOKENS}")
+
+
+def align_dp(b: Batch):
+    """Fused DP: returns device tensors (seg_start, seg_end, seg_score, t_start, status)."""
+    lib = load()
+    _validate(b)
+    dev = b.device
+    nt = max(b.tok_off[-1], 1)
+    seg_start = torch.empty(nt, dtype=torch.int32, device=dev)
+    seg_end = torch.empty(nt, dtype=torch.int32, device=dev)
+    seg_score = torch.empty(nt, dtype=torch.float64, device=dev)
+    t_start = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+    status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+    wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
+    ws = _ws.get(dev, wsb)
+    with torch.cuda.device(dev):
+        _check(lib.wx_align_dp(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank),
+                               b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end), _ptr(seg_score),
+                               _ptr(t_start), _ptr(status), _ptr(ws), wsb, _stream(dev)))
+    return seg_start, seg_end, seg_score, t_start, status
+
+
+def trellis(b: Batch):
+    """Materialised trellises (CSR): returns (flat tensor, offsets list)."""
+    lib = load()
+    _validate(b)
+    dev = b.device
+    offs = [0]
+    for T, N in zip(b.Ts, b.Ns):
+        offs.append(offs[-1] + (T + 1) * (N + 1))
+    out = torch.empty(max(offs[-1], 1), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib.wx_trellis(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank),
+                              b.S, b.max_N, _ptr(out), _ptr(_dev_i64(offs, dev)), _stream(dev)))
+    return out, offs
+
+
+def backtrack(b: Batch, tr_flat: torch.Tensor, tr_offs):
+    """backtrack() from materialised trellises: (path_tok, path_time, path_prob, path_len, t_start)."""
+    lib = load()
+    dev = b.device
+    cap = max(b.sum_T, 1)
+    pt = torch.empty(cap, dtype=torch.int32, device=dev)
+    pm = torch.empty(cap, dtype=torch.int32, device=dev)
+    pp = torch.empty(cap, dtype=torch.float32, device=dev)
+    plen = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+    ts = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+    wsb = lib.wx_backtrack_workspace_bytes(b.S, b.sum_T, b.max_N)
+    ws = _ws.get(dev, wsb)
+    with torch.cuda.device(dev):
+        _check(lib.wx_backtrack(_ptr(tr_flat), _ptr(_dev_i64(tr_offs, dev)), _ptr(b.em), _ptr(b.em_off_d), b.V,
+                                _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S, b.max_N, b.sum_T,
+                                _ptr(pt), _ptr(pm), _ptr(pp), _ptr(plen), _ptr(ts), _ptr(ws), wsb, _stream(dev)))
+    return pt, pm, pp, plen, ts
+
+
+def merge_repeats(path_tok, path_time, path_prob, path_off, path_len, device):
+    """merge_repeats over CSR paths (device tensors): (seg_tok, seg_start, seg_end, seg_score, seg_count)."""
+    lib = load()
+    dev = torch.device(device)
+    S = int(path_len.numel())
+    cap = max(int(path_tok.numel()), 1)
+    st = torch.empty(cap, dtype=torch.int32, device=dev)
+    ss = torch.empty(cap, dtype=torch.int32, device=dev)
+    se = torch.empty(cap, dtype=torch.int32, device=dev)
+    sc = torch.empty(cap, dtype=torch.float64, device=dev)
+    cnt = torch.empty(max(S, 1), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib.wx_merge_repeats(_ptr(path_tok), _ptr(path_time), _ptr(path_prob), _ptr(path_off), _ptr(path_len),
+                                    S, _ptr(st), _ptr(ss), _ptr(se), _ptr(sc), _ptr(cnt), _stream(dev)))
+    return st, ss, se, sc, cnt
+
+
+def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration: float,
+             pad_onset: float = 0.0, pad_offset: float = 0.0, device=None):
+    """Binarize score columns on the GPU.  scores_list: 1-D float32 arrays/tensors (one per
+    column); sw_geometry: [(start, step, duration)] per column.  Returns [(starts, ends)]
+    as float64 numpy arrays per column."""
+    import numpy as np
+    lib = load()
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    F = [int(len(s)) for s in scores_list]
+    f_off = [0]
+    for n in F:
+        f_off.append(f_off[-1] + n)
+    r_off = [0]
+    for n in F:
+        r_off.append(r_off[-1] + n + 1)
+    ys = torch.cat([torch.as_tensor(s, dtype=torch.float32).reshape(-1) for s in scores_list]) if F else torch.zeros(1)
+    ys = ys.to(dev)
+    g = torch.tensor(sw_geometry, dtype=torch.float64).reshape(-1, 3).to(dev)
+    st0, stp, dur = g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].contiguous()
+    rs = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
+    re = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
+    cnt = torch.empty(max(len(F), 1), dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib.wx_binarize(_ptr(ys), _ptr(_dev_i64(f_off, dev)), len(F), _ptr(st0), _ptr(stp), _ptr(dur),
+                               float(np.float32(onset)), float(np.float32(offset)), float(max_duration),
+                               float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(_dev_i64(r_off, dev)),
+                               _ptr(cnt), _stream(dev)))
+    cnt_h = cnt.cpu().numpy()
+    rs_h, re_h = rs.cpu().numpy(), re.cpu().numpy()
+    out = []
+    for i in range(len(F)):
+        n = int(cnt_h[i])
+        if n < 0:
+            raise WXError("binarize region buffer overflow")
+        out.append((rs_h[r_off[i]:r_off[i] + n], re_h[r_off[i]:r_off[i] + n]))
+    return out

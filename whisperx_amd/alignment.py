@@ -1,0 +1,549 @@
+"""Forced alignment for WhisperX on MI355X — drop-in for ``whisperx.alignment``.
+
+Same public API and semantics as the reference (NADOOIT/whisperX @ 2025-01-12,
+whisperx/alignment.py):
+
+  load_align_model(language_code, device, model_name=None, model_dir=None)   :64-97
+  align(transcript, model, align_model_metadata, audio, device, ...)           :100-354
+  get_trellis(emission, tokens, blank_id=0)                                   :359-379
+  backtrack(trellis, emission, tokens, blank_id=0)                            :387-421
+  merge_repeats(path, transcript)                                             :438-454
+  merge_words(segments, separator="|")                                        :456-470
+  Point, Segment                                                              :381-436
+
+What changes is where the work runs:
+  * The emission forward stays a PyTorch-ROCm model call, one per segment (padding a
+    batch would change wav2vec2's logits), queued back to back on the device with no
+    host round trip; log_softmax stays on the device.
+  * The whole DP for all segments of a call is ONE launch of the fused HIP kernel
+    (libwxalign.so: wx_align_dp): trellis recurrence with a 1-bit decision map,
+    argmax, backtrack and merge_repeats.  Only per-token (start, end, score) come back.
+  * The per-segment pandas aggregation (:282-347) is re-implemented with plain Python/
+    numpy, reproducing pandas' results (NaN-skipping min/max, numpy-summed means,
+    np.round on word scores, groupby sort/NaN-drop, interpolate_nans).
+There is no CPU fallback: without a HIP device the DP raises.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Callable, Iterable, List, Optional, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+from .audio import SAMPLE_RATE, load_audio
+from .types import AlignedTranscriptionResult, SingleAlignedSegment, SingleSegment, SingleWordSegment
+from .utils import interpolate_nans
+
+PUNKT_ABBREVIATIONS = ["dr", "vs", "mr", "mrs", "prof"]
+
+LANGUAGES_WITHOUT_SPACES = ["ja", "zh"]
+
+DEFAULT_ALIGN_MODELS_TORCH = {
+    "en": "WAV2VEC2_ASR_BASE_960H",
+    "fr": "VOXPOPULI_ASR_BASE_10K_FR",
+    "de": "VOXPOPULI_ASR_BASE_10K_DE",
+    "es": "VOXPOPULI_ASR_BASE_10K_ES",
+    "it": "VOXPOPULI_ASR_BASE_10K_IT",
+}
+
+DEFAULT_ALIGN_MODELS_HF = {
+    "ja": "jonatasgrosman/wav2vec2-large-xlsr-53-japanese",
+    "zh": "jonatasgrosman/wav2vec2-large-xlsr-53-chinese-zh-cn",
+    "nl": "jonatasgrosman/wav2vec2-large-xlsr-53-dutch",
+    "uk": "Yehor/wav2vec2-xls-r-300m-uk-with-small-lm",
+    "pt": "jonatasgrosman/wav2vec2-large-xlsr-53-portuguese",
+    "ar": "jonatasgrosman/wav2vec2-large-xlsr-53-arabic",
+    "cs": "comodoro/wav2vec2-xls-r-300m-cs-250",
+    "ru": "jonatasgrosman/wav2vec2-large-xlsr-53-russian",
+    "pl": "jonatasgrosman/wav2vec2-large-xlsr-53-polish",
+    "hu": "jonatasgrosman/wav2vec2-large-xlsr-53-hungarian",
+    "fi": "jonatasgrosman/wav2vec2-large-xlsr-53-finnish",
+    "fa": "jonatasgrosman/wav2vec2-large-xlsr-53-persian",
+    "el": "jonatasgrosman/wav2vec2-large-xlsr-53-greek",
+    "tr": "mpoyraz/wav2vec2-xls-r-300m-cv7-turkish",
+    "da": "saattrupdan/wav2vec2-xls-r-300m-ftspeech",
+    "he": "imvladikon/wav2vec2-xls-r-300m-hebrew",
+    "vi": "nguyenvulebinh/wav2vec2-base-vi",
+    "ko": "kresnik/wav2vec2-large-xlsr-korean",
+    "ur": "kingabzpro/wav2vec2-large-xls-r-300m-Urdu",
+    "te": "anuragshas/wav2vec2-large-xlsr-53-telugu",
+    "hi": "theainerd/Wav2Vec2-large-xlsr-hindi",
+    "ca": "softcatala/wav2vec2-large-xlsr-catala",
+    "ml": "gvs/wav2vec2-large-xlsr-malayalam",
+    "no": "NbAiLab/nb-wav2vec2-1b-bokmaal",
+    "nn": "NbAiLab/nb-wav2vec2-300m-nynorsk",
+    "sk": "comodoro/wav2vec2-xls-r-300m-sk-cv8",
+    "sl": "anton-l/wav2vec2-large-xlsr-53-slovenian",
+    "hr": "classla/wav2vec2-xls-r-parlaspeech-hr",
+}
+
+
+# ------------------------------------------------------------------------------- loading
+def load_align_model(language_code, device, model_name=None, model_dir=None):
+    """alignment.py:64-97.  torchaudio bundles when torchaudio is installed; otherwise a
+    Hugging Face Wav2Vec2ForCTC from a hub name or (offline) a local directory."""
+    if model_name is None:
+        if language_code in DEFAULT_ALIGN_MODELS_TORCH:
+            model_name = DEFAULT_ALIGN_MODELS_TORCH[language_code]
+        elif language_code in DEFAULT_ALIGN_MODELS_HF:
+            model_name = DEFAULT_ALIGN_MODELS_HF[language_code]
+        else:
+            print(f"There is no default alignment model set for this language ({language_code}).\
+                Please find a wav2vec2.0 model finetuned on this language in https://huggingface.co/models, then pass the model name in --align_model [MODEL_NAME]")
+            raise ValueError(f"No default align-model for language: {language_code}")
+
+    pipelines = _torchaudio_pipelines()
+    if model_name in pipelines:
+        import torchaudio
+
+        pipeline_type = "torchaudio"
+        bundle = torchaudio.pipelines.__dict__[model_name]
+        align_model = bundle.get_model(dl_kwargs={"model_dir": model_dir}).to(device)
+        labels = bundle.get_labels()
+        align_dictionary = {c.lower(): i for i, c in enumerate(labels)}
+    else:
+        try:
+            from transformers import Wav2Vec2ForCTC, Wav2Vec2Processor
+
+            processor = Wav2Vec2Processor.from_pretrained(model_name, cache_dir=model_dir)
+            align_model = Wav2Vec2ForCTC.from_pretrained(model_name, cache_dir=model_dir)
+        except Exception as e:
+            print(e)
+            print("Error loading model from huggingface, check https://huggingface.co/models for finetuned wav2vec2.0 models")
+            raise ValueError(f'The chosen align_model "{model_name}" could not be found in huggingface (https://huggingface.co/models) or torchaudio (https://pytorch.org/audio/stable/pipelines.html#id14)')
+        pipeline_type = "huggingface"
+        align_model = align_model.to(device)
+        align_dictionary = {char.lower(): code for char, code in processor.tokenizer.get_vocab().items()}
+
+    align_metadata = {"language": language_code, "dictionary": align_dictionary, "type": pipeline_type}
+    return align_model, align_metadata
+
+
+def _torchaudio_pipelines():
+    try:
+        import torchaudio  # noqa: F401
+
+        return set(torchaudio.pipelines.__all__)
+    except Exception:
+        return set()
+
+
+# ------------------------------------------------------------------------ sentence spans
+_sentence_splitter: Optional[Callable[[str], list]] = None
+
+
+def set_sentence_splitter(fn: Optional[Callable[[str], list]]):
+    """Override the sentence splitter (fn(text) -> [(start, end)]); None restores Punkt."""
+    global _sentence_splitter
+    _sentence_splitter = fn
+
+
+_punkt = None
+
+
+def _sentence_spans(text: str):
+    if _sentence_splitter is not None:
+        return list(_sentence_splitter(text))
+    global _punkt
+    if _punkt is None:
+        try:
+            from nltk.tokenize.punkt import PunktParameters, PunktSentenceTokenizer
+
+            params = PunktParameters()
+            params.abbrev_types = set(PUNKT_ABBREVIATIONS)
+            _punkt = PunktSentenceTokenizer(params)
+        except Exception:
+            _punkt = False
+    if _punkt:
+        return list(_punkt.span_tokenize(text))
+    # nltk absent: single-sentence span (NLTK's final slice for one sentence)
+    return [(0, len(text.rstrip()))]
+
+
+# ------------------------------------------------------------------------------- align()
+def _prepare(segment: dict, dictionary, lang: str):
+    """alignment.py:137-177: clean chars/indices, clean words, sentence spans (mutates)."""
+    text = segment["text"]
+    num_leading = len(text) - len(text.lstrip())
+    num_trailing = len(text) - len(text.rstrip())
+    per_word = text.split(" ") if lang not in LANGUAGES_WITHOUT_SPACES else text
+    spaces = lang not in LANGUAGES_WITHOUT_SPACES
+    last = len(text) - num_trailing - 1
+    clean_char, clean_cdx = [], []
+    for cdx in range(num_leading, last + 1):
+        c = text[cdx].lower()
+        if spaces:
+            c = c.replace(" ", "|")
+        if c in dictionary:
+            clean_char.append(c)
+            clean_cdx.append(cdx)
+    clean_wdx = [wdx for wdx, wrd in enumerate(per_word) if any(c in dictionary for c in wrd)]
+    segment["clean_char"] = clean_char
+    segment["clean_cdx"] = clean_cdx
+    segment["clean_wdx"] = clean_wdx
+    segment["sentence_spans"] = _sentence_spans(text)
+
+
+def _emission(model, model_type, waveform_segment, device):
+    """alignment.py:217-233 on the device; returns the [T, V] log-probabilities (on device)."""
+    if waveform_segment.shape[-1] < 400:
+        lengths = torch.as_tensor([waveform_segment.shape[-1]]).to(device)
+        waveform_segment = torch.nn.functional.pad(waveform_segment, (0, 400 - waveform_segment.shape[-1]))
+    else:
+        lengths = None
+    with torch.inference_mode():
+        if model_type == "torchaudio":
+            emissions, _ = model(waveform_segment.to(device), lengths=lengths)
+        elif model_type == "huggingface":
+            emissions = model(waveform_segment.to(device)).logits
+        else:
+            raise NotImplementedError(f"Align model of type {model_type} not supported.")
+        emissions = torch.log_softmax(emissions, dim=-1)
+    return emissions[0].detach()
+
+
+def _dp_device(device):
+    """Device on which the DP runs: the model's device if it is a HIP device, else GPU 0."""
+    d = torch.device(device) if not isinstance(device, torch.device) else device
+    if d.type == "cuda":
+        return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
+    if not torch.cuda.is_available():
+        raise _lib.WXError("whisperx_amd.align needs a HIP device for the alignment DP (no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def blank_id_of(dictionary) -> int:
+    """alignment.py:237-240 (the last '[pad]'/'<pad>' entry wins, default 0)."""
+    blank_id = 0
+    for char, code in dictionary.items():
+        if char == "[pad]" or char == "<pad>":
+            blank_id = code
+    return blank_id
+
+
+def align(
+    transcript: Iterable[SingleSegment],
+    model: torch.nn.Module,
+    align_model_metadata: dict,
+    audio: Union[str, np.ndarray, torch.Tensor],
+    device: str,
+    interpolate_method: str = "nearest",
+    return_char_alignments: bool = False,
+    print_progress: bool = False,
+    combined_progress: bool = False,
+) -> AlignedTranscriptionResult:
+    """Align phoneme recognition predictions to known transcription (alignment.py:100-354)."""
+    if not torch.is_tensor(audio):
+        if isinstance(audio, str):
+            audio = load_audio(audio)
+        audio = torch.from_numpy(audio)
+    if len(audio.shape) == 1:
+        audio = audio.unsqueeze(0)
+
+    MAX_DURATION = audio.shape[1] / SAMPLE_RATE
+
+    model_dictionary = align_model_metadata["dictionary"]
+    model_lang = align_model_metadata["language"]
+    model_type = align_model_metadata["type"]
+
+    # 1. text preparation (mutates the input segments like the reference)
+    total_segments = len(transcript)
+    for sdx, segment in enumerate(transcript):
+        if print_progress:
+            base_progress = ((sdx + 1) / total_segments) * 100
+            percent_complete = (50 + base_progress / 2) if combined_progress else base_progress
+            print(f"Progress: {percent_complete:.2f}%...")
+        _prepare(segment, model_dictionary, model_lang)
+
+    # 2a. emissions for every alignable segment, queued on the device
+    blank_id = blank_id_of(model_dictionary)
+    dp_dev = _dp_device(device)
+    plan = []  # per segment: ("skip", reason) | ("dp", index into batch)
+    ems, toks, blanks, meta = [], [], [], []
+    for sdx, segment in enumerate(transcript):
+        t1, t2 = segment["start"], segment["end"]
+        if len(segment["clean_char"]) == 0:
+            plan.append(("nochars", None))
+            continue
+        if t1 >= MAX_DURATION:
+            plan.append(("toolate", None))
+            continue
+        text_clean = "".join(segment["clean_char"])
+        tokens = [model_dictionary[c] for c in text_clean]
+        f1 = int(t1 * SAMPLE_RATE)
+        f2 = int(t2 * SAMPLE_RATE)
+        waveform_segment = audio[:, f1:f2]
+        em = _emission(model, model_type, waveform_segment, device)
+        plan.append(("dp", len(ems)))
+        ems.append(em)
+        toks.append(tokens)
+        blanks.append(blank_id)
+        meta.append((text_clean, waveform_segment.size(0)))
+
+    # 2b. one fused DP launch for all segments
+    results = _run_dp(ems, toks, blanks, dp_dev) if ems else []
+
+    # 2c. timestamps and aggregation, in segment order (same prints, same order)
+    aligned_segments: List[SingleAlignedSegment] = []
+    for sdx, segment in enumerate(transcript):
+        t1, t2, text = segment["start"], segment["end"], segment["text"]
+        aligned_seg: SingleAlignedSegment = {"start": t1, "end": t2, "text": text, "words": []}
+        if return_char_alignments:
+            aligned_seg["chars"] = []
+        kind, bi = plan[sdx]
+        if kind == "nochars":
+            print(f'Failed to align segment ("{segment["text"]}"): no characters in this segment found in model dictionary, resorting to original...')
+            aligned_segments.append(aligned_seg)
+            continue
+        if kind == "toolate":
+            print(f'Failed to align segment ("{segment["text"]}"): original start time longer than audio duration, skipping...')
+            aligned_segments.append(aligned_seg)
+            continue
+        ok, starts, ends, scores, T = results[bi]
+        if not ok:
+            print(f'Failed to align segment ("{segment["text"]}"): backtrack failed, resorting to original...')
+            aligned_segments.append(aligned_seg)
+            continue
+        _, n_channels = meta[bi]
+        aligned_segments += aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang,
+                                              interpolate_method, return_char_alignments)
+
+    word_segments: List[SingleWordSegment] = []
+    for segment in aligned_segments:
+        word_segments += segment["words"]
+    return {"segments": aligned_segments, "word_segments": word_segments}
+
+
+def _run_dp(ems, toks, blanks, dev):
+    batch = _lib.Batch(ems, toks, blanks, device=dev)
+    seg_start, seg_end, seg_score, t_start, status = _lib.align_dp(batch)
+    # one device->host copy of everything the host needs
+    ss = seg_start.cpu().numpy()
+    se = seg_end.cpu().numpy()
+    sc = seg_score.cpu().numpy()
+    st = status.cpu().numpy()
+    out = []
+    for i in range(batch.S):
+        a, b = batch.tok_off[i], batch.tok_off[i + 1]
+        out.append((st[i] == 0, ss[a:b], se[a:b], sc[a:b], batch.Ts[i]))
+    return out
+
+
+# ------------------------------------------------------------------ host post-processing
+def _nanmin(vals):
+    m = math.nan
+    for v in vals:
+        if v == v and (m != m or v < m):
+            m = v
+    return np.float64(m)
+
+
+def _nanmax(vals):
+    m = math.nan
+    for v in vals:
+        if v == v and (m != m or v > m):
+            m = v
+    return np.float64(m)
+
+
+def _nanmean(vals):
+    """pandas Series.mean(): NaNs zeroed, numpy (pairwise) sum, / non-NaN count."""
+    cnt = sum(1 for v in vals if v == v)
+    if cnt == 0:
+        return np.float64(math.nan)
+    arr = np.array([v if v == v else 0.0 for v in vals], dtype=np.float64)
+    return np.float64(arr.sum() / cnt)
+
+
+def aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang, interpolate_method,
+                      return_char_alignments):
+    """alignment.py:252-347 for one aligned segment: char timestamps, sentence/word records,
+    NaN interpolation and the (start, end) grouping.  Returns the list of sub-segments."""
+    t1, t2, text = segment["start"], segment["end"], segment["text"]
+    duration = t2 - t1
+    ratio = duration * n_channels / T
+    clean_pos = {cdx: i for i, cdx in enumerate(segment["clean_cdx"])}
+    no_spaces = model_lang in LANGUAGES_WITHOUT_SPACES
+    n = len(text)
+    c_start = [math.nan] * n
+    c_end = [math.nan] * n
+    c_score = [math.nan] * n
+    c_word = [0] * n
+    word_idx = 0
+    for cdx in range(n):
+        i = clean_pos.get(cdx)
+        if i is not None:
+            c_start[cdx] = round(int(starts[i]) * ratio + t1, 3)
+            c_end[cdx] = round(int(ends[i]) * ratio + t1, 3)
+            c_score[cdx] = round(float(scores[i]), 3)
+        c_word[cdx] = word_idx
+        if no_spaces:
+            word_idx += 1
+        elif cdx == n - 1 or text[cdx + 1] == " ":
+            word_idx += 1
+
+    subs = []
+    for (sstart, send) in segment["sentence_spans"]:
+        lo, hi = max(sstart, 0), min(send, n - 1)
+        rows = range(lo, hi + 1) if hi >= lo else range(0)
+        sentence_text = text[sstart:send]
+        sentence_start = _nanmin(c_start[r] for r in rows)
+        sentence_end = _nanmax(c_end[r] for r in rows if text[r] != " ")
+        words = []
+        seen = {}
+        order = []
+        for r in rows:
+            w = c_word[r]
+            if w not in seen:
+                seen[w] = []
+                order.append(w)
+            seen[w].append(r)
+        for w in order:
+            idx = seen[w]
+            word_text = "".join(text[r] for r in idx).strip()
+            if len(word_text) == 0:
+                continue
+            idx = [r for r in idx if text[r] != " "]
+            word_start = _nanmin(c_start[r] for r in idx)
+            word_end = _nanmax(c_end[r] for r in idx)
+            word_score = round(_nanmean([c_score[r] for r in idx]), 3)
+            rec = {"word": word_text}
+            if not np.isnan(word_start):
+                rec["start"] = word_start
+            if not np.isnan(word_end):
+                rec["end"] = word_end
+            if not np.isnan(word_score):
+                rec["score"] = word_score
+            words.append(rec)
+        sub = {"text": sentence_text, "start": sentence_start, "end": sentence_end, "words": words}
+        if return_char_alignments:
+            chars = []
+            for r in rows:
+                rec = {"char": text[r]}
+                for key, v in (("start", c_start[r]), ("end", c_end[r]), ("score", c_score[r])):
+                    v = -1.0 if v != v else v
+                    if v != -1:
+                        rec[key] = float(v)
+                chars.append(rec)
+            sub["chars"] = chars
+        subs.append(sub)
+
+    if not subs:
+        return []
+    starts_s = interpolate_nans([s["start"] for s in subs], interpolate_method)
+    ends_s = interpolate_nans([s["end"] for s in subs], interpolate_method)
+    # groupby(["start", "end"], sort=True, dropna=True) + agg, rows in original order per group
+    keyed = [(starts_s[i], ends_s[i], i) for i in range(len(subs)) if starts_s[i] == starts_s[i] and ends_s[i] == ends_s[i]]
+    keyed.sort(key=lambda k: (k[0], k[1]))
+    sep = "" if model_lang in LANGUAGES_WITHOUT_SPACES else " "
+    out = []
+    i = 0
+    while i < len(keyed):
+        j = i
+        while j < len(keyed) and keyed[j][0] == keyed[i][0] and keyed[j][1] == keyed[i][1]:
+            j += 1
+        members = sorted(k[2] for k in keyed[i:j])
+        rec = {"start": float(keyed[i][0]), "end": float(keyed[i][1]),
+               "text": sep.join(subs[m]["text"] for m in members),
+               "words": [w for m in members for w in subs[m]["words"]]}
+        if return_char_alignments:
+            rec["chars"] = [c for m in members for c in subs[m]["chars"]]
+        out.append(rec)
+        i = j
+    return out
+
+
+# ------------------------------------------------------------------- DP-level APIs
+@dataclass
+class Point:
+    token_index: int
+    time_index: int
+    score: float
+
+
+@dataclass
+class Segment:
+    label: str
+    start: int
+    end: int
+    score: float
+
+    def __repr__(self):
+        return f"{self.label}\t({self.score:4.2f}): [{self.start:5d}, {self.end:5d})"
+
+    @property
+    def length(self):
+        return self.end - self.start
+
+
+def _as_tokens(tokens):
+    if torch.is_tensor(tokens):
+        return [int(x) for x in tokens.reshape(-1).tolist()]
+    return [int(x) for x in tokens]
+
+
+def get_trellis(emission, tokens, blank_id=0):
+    """alignment.py:359-379 on the GPU.  Returns the [T+1, N+1] fp32 trellis on the
+    emission's device (a CPU emission gets a CPU trellis back)."""
+    em = emission if torch.is_tensor(emission) else torch.as_tensor(emission)
+    dev = em.device if em.is_cuda else _dp_device("cuda")
+    toks = _as_tokens(tokens)
+    b = _lib.Batch([em], [toks], [blank_id], device=dev)
+    flat, offs = _lib.trellis(b)
+    out = flat[: offs[1]].view(b.Ts[0] + 1, len(toks) + 1)
+    return out if em.is_cuda else out.cpu()
+
+
+def backtrack(trellis, emission, tokens, blank_id=0):
+    """alignment.py:387-421 on the GPU: list[Point] or None."""
+    em = emission if torch.is_tensor(emission) else torch.as_tensor(emission)
+    dev = em.device if em.is_cuda else _dp_device("cuda")
+    toks = _as_tokens(tokens)
+    b = _lib.Batch([em], [toks], [blank_id], device=dev)
+    tr = torch.as_tensor(trellis, dtype=torch.float32).to(dev).contiguous().reshape(-1)
+    pt, pm, pp, plen, ts = _lib.backtrack(b, tr, [0, tr.numel()])
+    L = int(plen[0].item())
+    if L < 0:
+        return None
+    tok_h = pt[:L].cpu().tolist()
+    time_h = pm[:L].cpu().tolist()
+    prob_h = pp[:L].cpu().tolist()
+    return [Point(a, t, p) for a, t, p in zip(tok_h, time_h, prob_h)]
+
+
+def merge_repeats(path, transcript):
+    """alignment.py:438-454 on the GPU (run-length grouping, fp64 left-to-right means of
+    the fp32 path probabilities, as backtrack() produces them)."""
+    if not path:
+        return []
+    dev = _dp_device("cuda")
+    pt = torch.tensor([p.token_index for p in path], dtype=torch.int32).to(dev)
+    pm = torch.tensor([p.time_index for p in path], dtype=torch.int32).to(dev)
+    pp = torch.tensor([p.score for p in path], dtype=torch.float32).to(dev)
+    off = torch.zeros(1, dtype=torch.int64).to(dev)
+    ln = torch.tensor([len(path)], dtype=torch.int32).to(dev)
+    st, ss, se, sc, cnt = _lib.merge_repeats(pt, pm, pp, off, ln, dev)
+    G = int(cnt[0].item())
+    st, ss, se, sc = st[:G].cpu().tolist(), ss[:G].cpu().tolist(), se[:G].cpu().tolist(), sc[:G].cpu().tolist()
+    return [Segment(transcript[a], s, e, c) for a, s, e, c in zip(st, ss, se, sc)]
+
+
+def merge_words(segments, separator="|"):
+    """alignment.py:456-470 (host; not on the align() path): words between separator
+    labels, score weighted by segment length."""
+    words = []
+    run = []
+    for seg in list(segments) + [None]:
+        if seg is None or seg.label == separator:
+            if run:
+                label = "".join(x.label for x in run)
+                num = sum(x.score * x.length for x in run)
+                den = sum(x.length for x in run)
+                words.append(Segment(label, run[0].start, run[-1].end, num / den))
+            run = []
+        else:
+            run.append(seg)
+    return words

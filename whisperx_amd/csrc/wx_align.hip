@@ -1,0 +1,998 @@
+// wx_align.hip — MI355X (gfx950 / CDNA4) kernels for WhisperX's forced-alignment DP and
+// VAD hysteresis, behind the C ABI of include/wx_align.h.
+//
+// Reference being replaced (file:line in NADOOIT/whisperX @ 2025-01-12):
+//   get_trellis    whisperx/alignment.py:359-379     -> trellis_kernel (materialising)
+//   backtrack      whisperx/alignment.py:387-421     -> bits_from_trellis_kernel + walk
+//   merge_repeats  whisperx/alignment.py:438-454     -> merge_repeats_kernel
+//   align() DP     whisperx/alignment.py:242-250     -> align_dp_kernel (fused, no trellis)
+//   Binarize       whisperx/vad.py:118-180           -> binarize_kernel
+//
+// Design:
+//   * One wave64 per segment.  The trellis recurrence is row-parallel: row t+1 depends only
+//     on row t, so lane g owns the C contiguous cells j = g*C+1 .. g*C+C and a time step is
+//     C independent add/add/max cells plus one DPP wave_shr:1 for the left neighbour of the
+//     lane's first cell.  The sequential depth is T steps; throughput comes from many
+//     segments (waves) in flight.
+//   * Emission rows are staged 32 at a time into LDS (row stride VS = 32 or 64 floats) by
+//     global_load_lds, double-buffered, so the per-cell gather em[t, tok[j-1]] is one
+//     conflict-free ds_read_b32 with a compile-time immediate row offset.
+//   * The fused kernel never writes the trellis.  The backtrack test at (t, j) is bit for
+//     bit the forward comparison that produced trellis[t, j] (`changed > stayed`), so the
+//     forward keeps one bit per cell per step: lane-local 32-step column words (v_cmp +
+//     v_addc, shift-in), stored as [block][slot][lane].  The walk reads a 64-cell x 32-step
+//     window of them per block into the wave's lanes and steps with v_readlane + scalar ops.
+//   * merge_repeats is rebuilt from the walk's per-token start frames: token k spans
+//     [start_k, start_{k+1}); its first frame carries exp(em[t, tok[k]]), the others
+//     exp(em[t, 0]) (index 0, as alignment.py:409), summed left to right in fp64.
+//
+// Numerics are the reference's torch-CPU semantics (this file is compiled with
+// -ffp-contract=off): fp32 adds, NaN-propagating max (v_maximum3_f32 == torch.maximum),
+// strict `>` with ties staying, first-max/NaN-first argmax, fp64-accumulated column 0.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/wx_align.h"
+
+#define WX_VERSION "0.1.0"
+
+namespace wx {
+
+constexpr int kWave = 64;
+constexpr int kChunk = 32;  // emission rows per LDS buffer == bits per column word
+constexpr int kUnroll = 8;  // time steps per unrolled group
+
+__device__ __forceinline__ float nan_max(float a, float b) {
+    // IEEE-754-2019 maximum (NaN-propagating): torch.maximum for non-zero-sign cases.
+    return __builtin_elementwise_maximum(a, b);
+}
+
+// w <- 2w + (c > s): strict compare (false when unordered), shifted into a column word.
+__device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
+    unsigned r;
+    asm("v_cmp_gt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %3, %3, vcc"
+        : "=v"(r)
+        : "v"(c), "v"(s), "v"(w)
+        : "vcc");
+    return r;
+}
+
+// Correctly rounded fp32 exp (the reference's torch-CPU exp is within 1 ULP of it).
+__device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
+
+__device__ __forceinline__ float dpp_shr1(float old_lane0, float v) {
+    // lane l <- v[l-1]; lane 0 keeps old_lane0 (bound_ctrl off).
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old_lane0), __builtin_bit_cast(int, v),
+                                           0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Cell values live in an ext_vector so that the one dynamic (wave-uniform) index of the
+// step — the slot holding column N — lowers to s_set_gpr_idx_on/v_mov instead of scratch.
+template <int C>
+using cellvec = float __attribute__((ext_vector_type(C)));
+
+struct SegDesc {
+    int64_t row0;  // first emission row
+    int T;
+    int64_t tok0;
+    int N;
+    int blank;
+};
+
+__device__ __forceinline__ SegDesc load_desc(const int64_t* em_off, const int64_t* tok_off, const int32_t* blank_id,
+                                             int seg) {
+    SegDesc d;
+    d.row0 = em_off[seg];
+    d.T = uniform((int)(em_off[seg + 1] - d.row0));
+    d.tok0 = tok_off[seg];
+    d.N = uniform((int)(tok_off[seg + 1] - d.tok0));
+    d.blank = uniform(blank_id[seg]);
+    return d;
+}
+
+// Stage emission rows [r0, r0+nrows) of a segment into LDS buffer `dst` (row stride VS
+// floats) with global_load_lds: one dword per lane, one instruction per row, lanes >= V
+// masked.  Asynchronous: the caller waits vmcnt before reading.
+template <int VS>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
+    const int lane = lane_id();
+    if (lane < V) {
+        for (int r = 0; r < nrows; ++r) {
+            const float* src = E + (int64_t)(r0 + r) * V + lane;
+            __builtin_amdgcn_global_load_lds(src, dst + r * VS, 4, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Column-0 value tr[t][0]: 0 / fp32(cumsum) / +inf in the last N rows (alignment.py:367-370).
+__device__ __forceinline__ float col0_value(int t, double acc, int T, int N) {
+    const bool inf_row = (N == 0) || (t >= T + 1 - N);
+    if (inf_row) return INFINITY;
+    return t == 0 ? 0.0f : (float)acc;
+}
+
+// ------------------------------------------------------------------------------------
+// Cell -> (lane, slot) layout of one segment.  G = ceil(N/C) lanes are used; the first
+// n_short of them own C-1 cells, the rest C cells, so that column N always sits in the
+// compile-time slot C-1 of lane G-1 (its value feeds the argmax every step without a
+// dynamic register index).  Lanes >= G and the spare slot C-1 of short lanes compute
+// harmless garbage: cells only ever feed cells to their right.
+struct Layout {
+    int C;        // cells per full lane
+    int G;        // lanes used
+    int n_short;  // leading lanes with C-1 cells
+
+    __host__ __device__ static Layout make(int C, int N) {
+        Layout L;
+        L.C = C;
+        L.G = (N + C - 1) / C;
+        const int n_full = N - L.G * (C - 1);
+        L.n_short = L.G - n_full;
+        return L;
+    }
+    // first cell (1-based) and cell count of lane g
+    __device__ __forceinline__ int first(int g) const {
+        return g < n_short ? g * (C - 1) + 1 : n_short * (C - 1) + (g - n_short) * C + 1;
+    }
+    __device__ __forceinline__ int count(int g) const { return g < n_short ? C - 1 : (g < G ? C : 0); }
+    // (lane, slot) of 0-based cell c
+    __device__ __forceinline__ void locate(int c, int& g, int& k) const {
+        const int cs = n_short * (C - 1);
+        if (c < cs) {
+            g = c / (C - 1);
+            k = c - g * (C - 1);
+        } else {
+            const int c2 = c - cs;
+            g = n_short + c2 / C;
+            k = c2 - (g - n_short) * C;
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// The trellis forward pass shared by the fused and the materialising kernels.
+//   MODE 0: fused — per-cell 32-step decision words -> bits, argmax of column N, q0 row.
+//   MODE 1: materialise — write every trellis row (get_trellis).
+template <int C, int VS, int MODE>
+struct Forward {
+    static constexpr int kRowBytes = VS * 4;
+
+    __device__ static void run(const SegDesc& d, const float* __restrict__ E, int V,
+                               const int32_t* __restrict__ tok,
+                               unsigned* __restrict__ bits,   // MODE 0: segment's bitmap
+                               float* __restrict__ q0,         // MODE 0: exp(em[t,0]) per row
+                               float* __restrict__ tr,         // MODE 1: trellis
+                               int* t_start_out, float* lds /* 2 * kChunk * VS */) {
+        const int lane = lane_id();
+        const int T = d.T, N = d.N;
+        const Layout L = Layout::make(C, N);
+        const int f = L.first(lane), cnt = L.count(lane);
+        const bool is_short = lane < L.n_short;
+        // per-slot LDS byte offsets of em[., tok[j-1]]
+        int toff[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            const int j = f + k;
+            int tk = (k < cnt && j <= N) ? tok[d.tok0 + j - 1] : 0;
+            tk = (tk >= 0 && tk < V) ? tk : 0;
+            toff[k] = tk * 4;
+        }
+        const int boff = d.blank * 4;
+        const int gN = uniform(L.G - 1);  // column N = slot C-1 of lane G-1
+
+        cellvec<C> cur;
+#pragma unroll
+        for (int k = 0; k < C; ++k) cur[k] = -INFINITY;  // row 0, columns 1..N
+        unsigned w[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) w[k] = 0u;
+
+        double acc = 0.0;
+        float col0 = col0_value(0, 0.0, T, N);
+        // argmax over column N (row 0 is -inf): first strict max; the first NaN wins outright
+        float best = -INFINITY;
+        int best_t = 0, nan_t = 0;
+
+        if (MODE == 1) {
+            if (lane == 0) tr[0] = col0;
+            for (int j = lane + 1; j <= N; j += kWave) tr[j] = -INFINITY;
+        }
+
+        const int nch = (T + kChunk - 1) / kChunk;
+        if (nch > 0) stage_rows<VS>(E, V, 0, min(kChunk, T), lds);
+        int t = 0;
+        for (int q = 0; q < nch; ++q) {
+            float* buf = lds + (q & 1) * kChunk * VS;
+            const int rows = min(kChunk, T - q * kChunk);
+            wait_vm();
+            __syncthreads();
+            if (q + 1 < nch) stage_rows<VS>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
+                                          lds + ((q + 1) & 1) * kChunk * VS);
+            if (MODE == 0 && lane < rows) q0[q * kChunk + lane] = exp_cr(buf[lane * VS]);
+            const char* bb = reinterpret_cast<const char*>(buf);
+            int r = 0;
+            // ---- unrolled groups of kUnroll steps with immediate LDS row offsets
+            for (; r + kUnroll <= rows; r += kUnroll) {
+                const char* gb = bb + r * kRowBytes;
+                const char* ga[C];
+#pragma unroll
+                for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    step(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best,
+                         best_t, nan_t, tr);
+                    ++t;
+                }
+            }
+            // ---- remainder steps (last partial group)
+            for (; r < rows; ++r) {
+                const char* gb = bb + r * kRowBytes;
+                const char* ga[C];
+#pragma unroll
+                for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
+                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best, best_t, nan_t, tr);
+                ++t;
+            }
+            if (MODE == 0) {
+                const int sh = kChunk - rows;  // keep bit 31 = first step of the block
+#pragma unroll
+                for (int k = 0; k < C; ++k) {
+                    bits[((int64_t)q * C + k) * kWave + lane] = (sh == 0) ? w[k] : (w[k] << sh);
+                    w[k] = 0u;
+                }
+            }
+        }
+        if (MODE == 0) {
+            const int bt = __builtin_amdgcn_readlane(best_t, gN);
+            const int nt = __builtin_amdgcn_readlane(nan_t, gN);
+            *t_start_out = nt > 0 ? nt : bt;
+        }
+    }
+
+    __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
+                                                cellvec<C>& cur, unsigned (&w)[C], double& acc, float& col0,
+                                                int t, int T, int N, int lane, bool is_short, int f, int cnt,
+                                                float& best, int& best_t, int& nan_t, float* __restrict__ tr) {
+        const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
+        const float e0 = *reinterpret_cast<const float*>(gb + ro);
+        float et[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
+        // last cell of the lane to the left (short lanes end at slot C-2)
+        const float src = (C > 1 && is_short) ? cur[C > 1 ? C - 2 : 0] : cur[C - 1];
+        const float left = dpp_shr1(col0, src);
+#pragma unroll
+        for (int k = C - 1; k >= 0; --k) {
+            const float s = cur[k] + eb;
+            const float c = (k == 0 ? left : cur[k > 0 ? k - 1 : 0]) + et[k];
+            if (MODE == 0) w[k] = shift_in(w[k], c, s);
+            cur[k] = nan_max(s, c);
+        }
+        acc += (double)e0;
+        col0 = col0_value(t + 1, acc, T, N);
+        if (MODE == 0) {
+            const float v = cur[C - 1];
+            const bool gt = v > best;
+            best_t = gt ? t + 1 : best_t;
+            best = gt ? v : best;
+            nan_t = (v != v && nan_t == 0) ? t + 1 : nan_t;
+        } else {
+            const int64_t W = (int64_t)N + 1;
+            float* row = tr + (int64_t)(t + 1) * W;
+            if (lane == 0) row[0] = col0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                const int j = f + k;
+                if (k < cnt && j <= N) row[j] = cur[k];
+            }
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// Backtrack walk over the decision bitmap (alignment.py:395-421).  Uniform control flow,
+// executed by the whole wave; `lay` maps cells to the bitmap's (lane, slot) words.
+// Records start[k] = first frame of token k (the frame where the path moved onto it).
+// Returns true on success (j reached 0), false where the reference returns None.
+__device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bits, const Layout& lay, int b, int A) {
+    const int jj = A - lane_id();
+    if (jj < 1) return 0u;
+    int g, k;
+    lay.locate(jj - 1, g, k);
+    return bits[((int64_t)b * lay.C + k) * kWave + g];
+}
+
+__device__ bool walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start,
+                     int32_t* __restrict__ start) {
+    if (t_start <= 0 || N <= 0) return false;
+    int j = N;
+    int u = t_start - 1;  // decision index = t - 1
+    int b = u >> 5;
+    int A = j;
+    unsigned win = load_window(bits, lay, b, A);
+    int An = A;
+    unsigned nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
+    const bool writer = lane_id() == 0;
+    while (true) {
+        const int lo = b << 5;
+        while (u >= lo) {
+            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, A - j);
+            if ((word >> (31 - (u & 31))) & 1u) {
+                if (writer) start[j - 1] = u;
+                --j;
+                if (j == 0) return true;
+            }
+            --u;
+        }
+        if (u < 0) return false;
+        --b;
+        win = nxt;
+        A = An;
+        An = j;
+        nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
+    }
+}
+
+// merge_repeats from per-token start frames (alignment.py:438-454 + the prob rule of :409).
+__device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* __restrict__ tok, int N, int t_start,
+                             const float* __restrict__ q0, const int32_t* __restrict__ start, int32_t* __restrict__ seg_end,
+                             double* __restrict__ seg_score) {
+    for (int k = lane_id(); k < N; k += kWave) {
+        const int s = start[k];
+        const int e = (k + 1 < N) ? start[k + 1] : t_start;
+        int tk = tok[k];
+        tk = (tk >= 0 && tk < V) ? tk : 0;
+        double sum = (double)exp_cr(E[(int64_t)s * V + tk]);
+        for (int x = s + 1; x < e; ++x) sum += (double)q0[x];
+        seg_end[k] = e;
+        seg_score[k] = sum / (double)(e - s);
+    }
+}
+
+__device__ __forceinline__ void block_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Cells-per-lane buckets (one kernel instantiation each).
+#define WX_CELL_BUCKETS(X) X(1) X(2) X(4) X(6) X(8) X(12) X(16) X(24) X(32)
+
+__host__ __device__ __forceinline__ int bucket_cells(int N) {
+    const int need = (N + kWave - 1) / kWave;
+    if (need <= 1) return 1;
+    if (need <= 2) return 2;
+    if (need <= 4) return 4;
+    if (need <= 6) return 6;
+    if (need <= 8) return 8;
+    if (need <= 12) return 12;
+    if (need <= 16) return 16;
+    if (need <= 24) return 24;
+    return 32;
+}
+
+struct AlignArgs {
+    const float* em;
+    const int64_t* em_off;
+    int V;
+    const int32_t* tok;
+    const int64_t* tok_off;
+    const int32_t* blank_id;
+    int S;
+    int32_t* seg_start;
+    int32_t* seg_end;
+    double* seg_score;
+    int32_t* t_start;
+    int32_t* status;
+    unsigned* bits;  // workspace: bitmap region
+    int bits_stride_cells;  // 64 * Cstride dwords per block
+    float* q0;       // workspace: sum_T floats
+};
+
+template <int C, int VS>
+__global__ __launch_bounds__(kWave) void align_dp_kernel(AlignArgs a) {
+    __shared__ float lds[2 * kChunk * VS];
+    const int seg = blockIdx.x;
+    const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
+    if (bucket_cells(d.N) != C) return;  // another instantiation owns this segment
+    const int lane = lane_id();
+    if (d.N <= 0 || d.T <= 0) {
+        if (lane == 0) {
+            a.t_start[seg] = 0;
+            a.status[seg] = 1;
+        }
+        return;
+    }
+    const float* E = a.em + d.row0 * a.V;
+    unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
+    float* q0 = a.q0 + d.row0;
+    int ts = 0;
+    Forward<C, VS, 0>::run(d, E, a.V, a.tok, bits, q0, nullptr, &ts, lds);
+    if (lane == 0) a.t_start[seg] = ts;
+    block_fence();
+    int32_t* start = a.seg_start + d.tok0;
+    const bool ok = walk(bits, Layout::make(C, d.N), d.N, ts, start);
+    if (lane == 0) a.status[seg] = ok ? 0 : 1;
+    if (!ok) return;
+    block_fence();
+    merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
+}
+
+struct TrellisArgs {
+    const float* em;
+    const int64_t* em_off;
+    int V;
+    const int32_t* tok;
+    const int64_t* tok_off;
+    const int32_t* blank_id;
+    float* tr;
+    const int64_t* tr_off;
+};
+
+template <int C, int VS>
+__global__ __launch_bounds__(kWave) void trellis_kernel(TrellisArgs a) {
+    __shared__ float lds[2 * kChunk * VS];
+    const int seg = blockIdx.x;
+    const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
+    if (bucket_cells(d.N) != C) return;
+    float* tr = a.tr + a.tr_off[seg];
+    const int lane = lane_id();
+    if (d.N == 0) {  // the whole single column is +inf (alignment.py:369-370 with num_tokens = 0)
+        for (int t = lane; t <= d.T; t += kWave) tr[t] = INFINITY;
+        return;
+    }
+    const float* E = a.em + d.row0 * a.V;
+    Forward<C, VS, 1>::run(d, E, a.V, a.tok, nullptr, nullptr, tr, nullptr, lds);
+}
+
+// ------------------------------------------------------------------------------------
+// backtrack() from a materialised trellis: recompute the decision bits from the trellis
+// (one column word per thread: 32 rows of one cell), argmax of column N, shared walk,
+// then expand the per-token spans into the reference's Point list.
+struct BacktrackArgs {
+    const float* tr;
+    const int64_t* tr_off;
+    const float* em;
+    const int64_t* em_off;
+    int V;
+    const int32_t* tok;
+    const int64_t* tok_off;
+    const int32_t* blank_id;
+    int32_t* path_tok;
+    int32_t* path_time;
+    float* path_prob;
+    int32_t* path_len;
+    int32_t* t_start;
+    unsigned* bits;
+    int bits_stride_cells;
+    int32_t* start;  // workspace: per-token start frames (CSR by tok_off)
+};
+
+__global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
+    const int seg = blockIdx.x;
+    const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
+    const int T = d.T, N = d.N;
+    const float* tr = a.tr + a.tr_off[seg];
+    const float* E = a.em + d.row0 * a.V;
+    const int32_t* tok = a.tok + d.tok0;
+    const int64_t W = (int64_t)N + 1;
+    const int cpl = max(1, (N + kWave - 1) / kWave);
+    unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
+    const int nblk = (T + kChunk - 1) / kChunk;
+    // (1) decision words: word (b, cell j) bit 31-s = changed>stayed at decision u = 32b+s
+    const int nwords = nblk * cpl * kWave;
+    for (int i = threadIdx.x; i < nwords; i += blockDim.x) {
+        const int g = i % kWave;
+        const int k = (i / kWave) % cpl;
+        const int b = i / (kWave * cpl);
+        const int j = g * cpl + k + 1;
+        unsigned wv = 0u;
+        if (j <= N) {
+            int tk = tok[j - 1];
+            tk = (tk >= 0 && tk < a.V) ? tk : 0;
+            for (int s = 0; s < kChunk; ++s) {
+                const int u = b * kChunk + s;
+                unsigned bit = 0u;
+                if (u < T) {
+                    const float stayed = tr[(int64_t)u * W + j] + E[(int64_t)u * a.V + d.blank];
+                    const float changed = tr[(int64_t)u * W + j - 1] + E[(int64_t)u * a.V + tk];
+                    bit = changed > stayed ? 1u : 0u;
+                }
+                wv = (wv << 1) | bit;
+            }
+        }
+        bits[((int64_t)b * cpl + k) * kWave + g] = wv;
+    }
+    // (2) argmax of column N over rows 0..T (first max, NaN counts as max)
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    bool bn = false;
+    for (int t = threadIdx.x; t <= T; t += blockDim.x) {
+        const float v = tr[(int64_t)t * W + N];
+        if (bn) continue;
+        if (v != v) {
+            bn = true;
+            bv = v;
+            bi = t;
+        } else if (bi == 0x7fffffff || v > bv) {
+            bv = v;
+            bi = t;
+        }
+    }
+    sv[threadIdx.x] = bn ? NAN : bv;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) {
+            const float v1 = sv[threadIdx.x], v2 = sv[threadIdx.x + off];
+            const int i1 = si[threadIdx.x], i2 = si[threadIdx.x + off];
+            const bool n1 = v1 != v1 && i1 != 0x7fffffff, n2 = v2 != v2 && i2 != 0x7fffffff;
+            bool take2;
+            if (i2 == 0x7fffffff) take2 = false;
+            else if (i1 == 0x7fffffff) take2 = true;
+            else if (n1 && n2) take2 = i2 < i1;
+            else if (n1) take2 = false;
+            else if (n2) take2 = true;
+            else if (v2 > v1) take2 = true;
+            else if (v1 > v2) take2 = false;
+            else take2 = i2 < i1;
+            if (take2) {
+                sv[threadIdx.x] = v2;
+                si[threadIdx.x] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    const int ts = (N == 0) ? 0 : si[0];
+    if (threadIdx.x == 0) a.t_start[seg] = ts;
+    __threadfence_block();
+    __syncthreads();
+    // (3) walk (wave 0)
+    int32_t* start = a.start + d.tok0;
+    __shared__ int ok_sh;
+    if (threadIdx.x < kWave) {
+        Layout lay;
+        lay.C = cpl;
+        lay.G = kWave;
+        lay.n_short = 0;
+        const bool ok = walk(bits, lay, N, ts, start);
+        if (threadIdx.x == 0) ok_sh = ok ? 1 : 0;
+    }
+    __threadfence_block();
+    __syncthreads();
+    const bool ok = ok_sh != 0;
+    if (threadIdx.x == 0) a.path_len[seg] = ok ? (ts - start[0]) : -1;
+    if (!ok) return;
+    // (4) expand spans -> Points (forward order) at path offset em_off[seg]
+    const int base_t = start[0];
+    int32_t* ptok = a.path_tok + d.row0;
+    int32_t* ptime = a.path_time + d.row0;
+    float* pprob = a.path_prob + d.row0;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const int s = start[k];
+        const int e = (k + 1 < N) ? start[k + 1] : ts;
+        int tk = tok[k];
+        tk = (tk >= 0 && tk < a.V) ? tk : 0;
+        for (int x = s; x < e; ++x) {
+            ptok[x - base_t] = k;
+            ptime[x - base_t] = x;
+            pprob[x - base_t] = exp_cr(E[(int64_t)x * a.V + (x == s ? tk : 0)]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// merge_repeats over arbitrary paths: run boundaries by ballot, then one fp64 left-to-right
+// sum per run.  One wave per path.
+struct MergeArgs {
+    const int32_t* ptok;
+    const int32_t* ptime;
+    const float* pprob;
+    const int64_t* path_off;
+    const int32_t* path_len;
+    int32_t* seg_tok;
+    int32_t* seg_start;
+    int32_t* seg_end;
+    double* seg_score;
+    int32_t* seg_count;
+};
+
+__global__ __launch_bounds__(kWave) void merge_repeats_kernel(MergeArgs a) {
+    const int seg = blockIdx.x;
+    const int lane = lane_id();
+    const int L = uniform(a.path_len[seg]);
+    if (L <= 0) {
+        if (lane == 0) a.seg_count[seg] = 0;
+        return;
+    }
+    const int64_t off = a.path_off[seg];
+    const int32_t* pt = a.ptok + off;
+    const int32_t* pm = a.ptime + off;
+    const float* pp = a.pprob + off;
+    int32_t* gstart = a.seg_end + off;  // scratch: run start indices, overwritten below
+    int G = 0;
+    for (int i0 = 0; i0 < L; i0 += kWave) {
+        const int i = i0 + lane;
+        bool flag = false;
+        if (i < L) flag = (i == 0) || (pt[i] != pt[i - 1]);
+        const unsigned long long m = __ballot(flag);
+        const int pos = G + __popcll(m & ((1ull << lane) - 1ull));
+        if (flag) gstart[pos] = i;
+        G += __popcll(m);
+    }
+    wait_vm();
+    block_fence();
+    for (int g0 = 0; g0 < G; g0 += kWave) {
+        const int g = g0 + lane;
+        int i1 = 0, i2 = 0;
+        if (g < G) {
+            i1 = gstart[g];
+            i2 = (g + 1 < G) ? gstart[g + 1] : L;
+        }
+        wait_vm();
+        block_fence();
+        if (g < G) {
+            double sum = 0.0;
+            for (int i = i1; i < i2; ++i) sum += (double)pp[i];
+            a.seg_tok[off + g] = pt[i1];
+            a.seg_start[off + g] = pm[i1];
+            a.seg_end[off + g] = pm[i2 - 1] + 1;
+            a.seg_score[off + g] = sum / (double)(i2 - i1);
+        }
+        wait_vm();
+        block_fence();
+    }
+    if (lane == 0) a.seg_count[seg] = G;
+}
+
+// ------------------------------------------------------------------------------------
+// Binarize (vad.py:118-180), one wave per score column.  Event driven: the wave scans 256
+// frames per iteration for the next transition (ballot + ffs) instead of stepping the FSM
+// frame by frame; a min-cut split takes a wave argmin over the second half of the current
+// score list.  The score list is [stale?] + frames [lo, i): the reference keeps one stale
+// element (the deactivation frame, or frame 0) in front of the frames appended while active.
+struct BinarizeArgs {
+    const float* y;
+    const int64_t* f_off;
+    const double* sw_start;
+    const double* sw_step;
+    const double* sw_dur;
+    float onset, offset;
+    double maxd, pad_on, pad_off;
+    double* rs;
+    double* re;
+    const int64_t* reg_off;
+    int64_t* reg_count;
+};
+
+__device__ __forceinline__ double sw_mid(double st, double step, double dur, int64_t i) {
+    const double s = st + (double)i * step;
+    const double e = s + dur;
+    return 0.5 * (s + e);
+}
+
+// (value, frame) argmin with the reference's np.argmin semantics over increasing frames:
+// first NaN wins, else the first minimum.
+__device__ __forceinline__ void argmin_combine(float& v, int64_t& f, bool& nan, float v2, int64_t f2, bool nan2) {
+    if (f2 < 0) return;
+    if (f < 0) {
+        v = v2; f = f2; nan = nan2;
+        return;
+    }
+    bool take;
+    if (nan && nan2) take = f2 < f;
+    else if (nan) take = false;
+    else if (nan2) take = true;
+    else if (v2 < v) take = true;
+    else if (v < v2) take = false;
+    else take = f2 < f;
+    if (take) {
+        v = v2; f = f2; nan = nan2;
+    }
+}
+
+__global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
+    const int file = blockIdx.x;
+    const int lane = lane_id();
+    const int64_t f0 = a.f_off[file];
+    const int64_t F = a.f_off[file + 1] - f0;
+    const float* y = a.y + f0;
+    const double st = a.sw_start[file], step = a.sw_step[file], dur = a.sw_dur[file];
+    const int64_t r0 = a.reg_off[file];
+    const int64_t cap = a.reg_off[file + 1] - r0;
+    double* rs = a.rs + r0;
+    double* re = a.re + r0;
+    int64_t n = 0;
+    bool overflow = false;
+    auto emit = [&](double s, double e) {
+        if (!((e - s) > 1e-6)) return;  // pyannote Segment truthiness: empty segments are not stored
+        if (n >= cap) {
+            overflow = true;
+            return;
+        }
+        if (lane == 0) {
+            rs[n] = s;
+            re[n] = e;
+        }
+        ++n;
+    };
+    if (F <= 0) {
+        if (lane == 0) a.reg_count[file] = 0;
+        return;
+    }
+    double start = sw_mid(st, step, dur, 0);
+    bool active = y[0] > a.onset;
+    bool has_stale = !active;  // curr = [0]: stale when inactive, else the range [0, 1)
+    int64_t stale = 0;
+    int64_t lo = active ? 0 : 1;
+    int64_t i = 1;
+    while (i < F) {
+        // ---- find the next event frame e >= i
+        int64_t ev = -1;
+        bool split = false;
+        for (int64_t base = i; base < F && ev < 0; base += 4 * kWave) {
+            unsigned long long m[4];
+            unsigned long long ms[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t f = base + q * kWave + lane;
+                bool p = false, ps = false;
+                if (f < F) {
+                    const float v = y[f];
+                    if (!active) {
+                        p = v > a.onset;
+                    } else {
+                        ps = (sw_mid(st, step, dur, f) - start) > a.maxd;
+                        p = ps || (v < a.offset);
+                    }
+                }
+                m[q] = __ballot(p);
+                ms[q] = __ballot(ps);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (ev < 0 && m[q]) {
+                    const int l = __ffsll((long long)m[q]) - 1;
+                    ev = base + q * kWave + l;
+                    split = (ms[q] >> l) & 1ull;
+                }
+            }
+        }
+        if (ev < 0) break;
+        const double tev = sw_mid(st, step, dur, ev);
+        if (!active) {
+            start = tev;
+            active = true;
+            lo = ev + 1;  // the activation frame itself is not appended (vad.py:171-175)
+            i = ev + 1;
+            continue;
+        }
+        if (split) {
+            // curr = [stale?] + frames [lo, ev); search positions [len/2, len)
+            const int64_t len = (has_stale ? 1 : 0) + (ev - lo);
+            const int64_t sa = len / 2;
+            float bv = 0.f;
+            int64_t bf = -1;
+            bool bn = false;
+            const int64_t fa = lo + max<int64_t>(sa - (has_stale ? 1 : 0), 0);
+            for (int64_t f = fa + lane; f < ev; f += kWave) {
+                const float v = y[f];
+                argmin_combine(bv, bf, bn, v, f, v != v);
+            }
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const float v2 = __shfl_xor(bv, off);
+                const int64_t f2 = __shfl_xor(bf, off);
+                const bool n2 = __shfl_xor((int)bn, off) != 0;
+                argmin_combine(bv, bf, bn, v2, f2, n2);
+            }
+            int64_t cut = bf;
+            bool cut_is_stale = false;
+            if (has_stale && sa == 0) {  // position 0 (the stale element) is a candidate and comes first
+                const float sv = y[stale];
+                const bool sn = sv != sv;
+                if (bf < 0 || sn || (!bn && !(bv < sv))) {
+                    cut = stale;
+                    cut_is_stale = true;
+                }
+            }
+            const double mt = sw_mid(st, step, dur, cut);
+            emit(start - a.pad_on, mt + a.pad_off);
+            start = mt;
+            if (!cut_is_stale) lo = cut + 1;
+            has_stale = false;
+            i = ev + 1;  // frame ev appended: range becomes [lo, ev+1)
+        } else {
+            emit(start - a.pad_on, tev + a.pad_off);
+            start = tev;
+            active = false;
+            has_stale = true;
+            stale = ev;
+            i = ev + 1;
+        }
+    }
+    if (active) {
+        const double tl = (F == 1) ? sw_mid(st, step, dur, 0) : sw_mid(st, step, dur, F - 1);
+        emit(start - a.pad_on, tl + a.pad_off);
+    }
+    if (lane == 0) a.reg_count[file] = overflow ? -1 : n;
+}
+
+}  // namespace wx
+
+// ======================================================================================
+// C ABI
+using namespace wx;
+
+namespace {
+
+int launch_status() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// bitmap: per segment (floor(row0/32) + seg) block offsets, 64 * C_stride dwords per block
+size_t bitmap_bytes(int32_t S, int64_t sum_T, int64_t max_N, int* stride_cells) {
+    const int C = bucket_cells((int)std::max<int64_t>(max_N, 1));
+    if (stride_cells) *stride_cells = kWave * C;
+    const int64_t blocks = sum_T / kChunk + S + 1;
+    return align_up((size_t)blocks * (size_t)kWave * (size_t)C * 4u, 256);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wx_version(void) { return WX_VERSION " gfx950"; }
+
+const char* wx_strerror(int code) {
+    switch (code) {
+        case WX_OK: return "ok";
+        case WX_E_INVALID: return "invalid argument";
+        case WX_E_VOCAB: return "vocabulary size outside [1, 64]";
+        case WX_E_TOO_LONG: return "segment has more than 2048 tokens";
+        case WX_E_WORKSPACE: return "workspace too small";
+        case WX_E_LAUNCH: return "kernel launch failed";
+        default: return hipGetErrorString((hipError_t)code);
+    }
+}
+
+size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
+    return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256);
+}
+
+int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
+                const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T, int32_t* seg_start,
+                int32_t* seg_end, double* seg_score, int32_t* t_start, int32_t* status, void* workspace,
+                size_t workspace_bytes, void* stream) {
+    if (S < 0 || sum_T < 0 || min_N < 0 || max_N < min_N) return WX_E_INVALID;
+    if (S == 0) return WX_OK;
+    if (!em || !em_off || !tok_off || !blank_id || !seg_start || !seg_end || !seg_score || !t_start || !status ||
+        !workspace)
+        return WX_E_INVALID;
+    if (V < 1 || V > WX_MAX_VOCAB) return WX_E_VOCAB;
+    if (max_N > WX_MAX_TOKENS) return WX_E_TOO_LONG;
+    if (workspace_bytes < wx_align_dp_workspace_bytes(S, sum_T, max_N)) return WX_E_WORKSPACE;
+    AlignArgs a;
+    a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id; a.S = S;
+    a.seg_start = seg_start; a.seg_end = seg_end; a.seg_score = seg_score; a.t_start = t_start; a.status = status;
+    const size_t bm = bitmap_bytes(S, sum_T, max_N, &a.bits_stride_cells);
+    a.bits = reinterpret_cast<unsigned*>(workspace);
+    a.q0 = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + bm);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int lo = bucket_cells((int)std::max<int64_t>(min_N, 1)), hi = bucket_cells((int)std::max<int64_t>(max_N, 1));
+    const dim3 grid(S), block(kWave);
+    // N == 0 segments belong to the C=1 bucket (bucket_cells(0) == 1) and are handled there.
+    const int lo_eff = (min_N == 0) ? 1 : lo;
+#define WX_LAUNCH_ALIGN(CC)                                                                       \
+    if (CC >= lo_eff && CC <= hi) {                                                               \
+        if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32>), grid, block, 0, st, a);       \
+        else hipLaunchKernelGGL((align_dp_kernel<CC, 64>), grid, block, 0, st, a);               \
+    }
+    WX_CELL_BUCKETS(WX_LAUNCH_ALIGN)
+#undef WX_LAUNCH_ALIGN
+    return launch_status();
+}
+
+int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
+               const int32_t* blank_id, int32_t S, int64_t max_N, float* trellis, const int64_t* tr_off,
+               void* stream) {
+    if (S < 0 || max_N < 0) return WX_E_INVALID;
+    if (S == 0) return WX_OK;
+    if (!em || !em_off || !tok_off || !blank_id || !trellis || !tr_off) return WX_E_INVALID;
+    if (V < 1 || V > WX_MAX_VOCAB) return WX_E_VOCAB;
+    if (max_N > WX_MAX_TOKENS) return WX_E_TOO_LONG;
+    TrellisArgs a;
+    a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id;
+    a.tr = trellis; a.tr_off = tr_off;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int hi = bucket_cells((int)std::max<int64_t>(max_N, 1));
+    const dim3 grid(S), block(kWave);
+#define WX_LAUNCH_TR(CC)                                                                          \
+    if (CC <= hi) {                                                                               \
+        if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32>), grid, block, 0, st, a);        \
+        else hipLaunchKernelGGL((trellis_kernel<CC, 64>), grid, block, 0, st, a);                \
+    }
+    WX_CELL_BUCKETS(WX_LAUNCH_TR)
+#undef WX_LAUNCH_TR
+    return launch_status();
+}
+
+size_t wx_backtrack_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
+    const int64_t cpl = std::max<int64_t>(1, (max_N + kWave - 1) / kWave);
+    const int64_t blocks = sum_T / kChunk + S + 1;
+    // bitmap + per-token start frames (sum of N <= S * max_N)
+    return align_up((size_t)blocks * kWave * (size_t)cpl * 4u, 256) + align_up((size_t)(S * max_N + 1) * 4u, 256);
+}
+
+int wx_backtrack(const float* trellis, const int64_t* tr_off, const float* em, const int64_t* em_off, int32_t V,
+                 const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id, int32_t S, int64_t max_N,
+                 int64_t sum_T, int32_t* path_tok, int32_t* path_time, float* path_prob, int32_t* path_len,
+                 int32_t* t_start, void* workspace, size_t workspace_bytes, void* stream) {
+    if (S < 0 || max_N < 0 || sum_T < 0) return WX_E_INVALID;
+    if (S == 0) return WX_OK;
+    if (!trellis || !tr_off || !em || !em_off || !tok_off || !blank_id || !path_tok || !path_time || !path_prob ||
+        !path_len || !t_start || !workspace)
+        return WX_E_INVALID;
+    if (V < 1) return WX_E_VOCAB;
+    if (workspace_bytes < wx_backtrack_workspace_bytes(S, sum_T, max_N)) return WX_E_WORKSPACE;
+    BacktrackArgs a;
+    a.tr = trellis; a.tr_off = tr_off; a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off;
+    a.blank_id = blank_id; a.path_tok = path_tok; a.path_time = path_time; a.path_prob = path_prob;
+    a.path_len = path_len; a.t_start = t_start;
+    const int64_t cpl = std::max<int64_t>(1, (max_N + kWave - 1) / kWave);
+    a.bits_stride_cells = (int)(kWave * cpl);
+    const int64_t blocks = sum_T / kChunk + S + 1;
+    const size_t bm = align_up((size_t)blocks * kWave * (size_t)cpl * 4u, 256);
+    a.bits = reinterpret_cast<unsigned*>(workspace);
+    a.start = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(workspace) + bm);
+    hipLaunchKernelGGL(backtrack_kernel, dim3(S), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
+
+int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const float* path_prob,
+                     const int64_t* path_off, const int32_t* path_len, int32_t S, int32_t* seg_tok,
+                     int32_t* seg_start, int32_t* seg_end, double* seg_score, int32_t* seg_count, void* stream) {
+    if (S < 0) return WX_E_INVALID;
+    if (S == 0) return WX_OK;
+    if (!path_tok || !path_time || !path_prob || !path_off || !path_len || !seg_tok || !seg_start || !seg_end ||
+        !seg_score || !seg_count)
+        return WX_E_INVALID;
+    MergeArgs a;
+    a.ptok = path_tok; a.ptime = path_time; a.pprob = path_prob; a.path_off = path_off; a.path_len = path_len;
+    a.seg_tok = seg_tok; a.seg_start = seg_start; a.seg_end = seg_end; a.seg_score = seg_score;
+    a.seg_count = seg_count;
+    hipLaunchKernelGGL(merge_repeats_kernel, dim3(S), dim3(kWave), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
+
+int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, const double* sw_start,
+                const double* sw_step, const double* sw_duration, float onset, float offset, double max_duration,
+                double pad_onset, double pad_offset, double* reg_start, double* reg_end, const int64_t* reg_off,
+                int64_t* reg_count, void* stream) {
+    if (n_files < 0) return WX_E_INVALID;
+    if (n_files == 0) return WX_OK;
+    if (!scores || !f_off || !sw_start || !sw_step || !sw_duration || !reg_start || !reg_end || !reg_off ||
+        !reg_count)
+        return WX_E_INVALID;
+    BinarizeArgs a;
+    a.y = scores; a.f_off = f_off; a.sw_start = sw_start; a.sw_step = sw_step; a.sw_dur = sw_duration;
+    a.onset = onset; a.offset = offset; a.maxd = max_duration; a.pad_on = pad_onset; a.pad_off = pad_offset;
+    a.rs = reg_start; a.re = reg_end; a.reg_off = reg_off; a.reg_count = reg_count;
+    hipLaunchKernelGGL(binarize_kernel, dim3(n_files), dim3(kWave), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
+
+}  // extern "C"
