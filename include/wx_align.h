@@ -50,7 +50,7 @@ enum {
 };
 
 #define WX_MAX_VOCAB 64      /* emission columns held in LDS per row */
-#define WX_MAX_TOKENS 2048   /* tokens per segment (64 lanes x 32 cells) */
+#define WX_MAX_TOKENS 16384  /* tokens per segment (8 waves x 64 lanes x 32 cells) */
 
 const char* wx_version(void);
 const char* wx_strerror(int code);

@@ -61,7 +61,7 @@ def test_argument_validation_without_device(lib):
     dummy = ctypes.c_void_p(8)
     assert lib.wx_align_dp(dummy, dummy, 100, dummy, dummy, dummy, 1, 1, 1, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 1 << 30, None) == 1002
-    assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 5000, 10, dummy, dummy, dummy, dummy,
+    assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 20000, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 1 << 30, None) == 1003
     assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 10, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 16, None) == 1004

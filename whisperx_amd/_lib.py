@@ -21,7 +21,7 @@ SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 MAX_VOCAB = 64
-MAX_TOKENS = 2048
+MAX_TOKENS = 16384
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

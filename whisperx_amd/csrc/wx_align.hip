@@ -101,7 +101,7 @@ __device__ __forceinline__ SegDesc load_desc(const int64_t* em_off, const int64_
 // masked.  Asynchronous: the caller waits vmcnt before reading.
 template <int VS>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
-    const int lane = lane_id();
+    const int lane = (int)threadIdx.x;  // wave 0 stages for the whole workgroup
     if (lane < V) {
         for (int r = 0; r < nrows; ++r) {
             const float* src = E + (int64_t)(r0 + r) * V + lane;
@@ -129,10 +129,12 @@ struct Layout {
     int C;        // cells per full lane
     int G;        // lanes used
     int n_short;  // leading lanes with C-1 cells
+    int lanes;    // lanes of the workgroup (bitmap word stride)
 
-    __host__ __device__ static Layout make(int C, int N) {
+    __host__ __device__ static Layout make(int C, int N, int lanes) {
         Layout L;
         L.C = C;
+        L.lanes = lanes;
         L.G = (N + C - 1) / C;
         const int n_full = N - L.G * (C - 1);
         L.n_short = L.G - n_full;
@@ -161,19 +163,22 @@ struct Layout {
 // The trellis forward pass shared by the fused and the materialising kernels.
 //   MODE 0: fused — per-cell 32-step decision words -> bits, argmax of column N, q0 row.
 //   MODE 1: materialise — write every trellis row (get_trellis).
-template <int C, int VS, int MODE>
+template <int C, int VS, int MODE, int W>
 struct Forward {
     static constexpr int kRowBytes = VS * 4;
+    static constexpr int kLanes = kWave * W;
 
     __device__ static void run(const SegDesc& d, const float* __restrict__ E, int V,
                                const int32_t* __restrict__ tok,
                                unsigned* __restrict__ bits,   // MODE 0: segment's bitmap
                                float* __restrict__ q0,         // MODE 0: exp(em[t,0]) per row
                                float* __restrict__ tr,         // MODE 1: trellis
-                               int* t_start_out, float* lds /* 2 * kChunk * VS */) {
-        const int lane = lane_id();
+                               int* t_start_out, float* lds /* 2 * kChunk * VS */,
+                               float* xch /* 2 * W: cross-wave neighbour exchange */,
+                               int* tsb /* t_start broadcast */) {
+        const int lane = (int)threadIdx.x;  // lane within the workgroup (W waves)
         const int T = d.T, N = d.N;
-        const Layout L = Layout::make(C, N);
+        const Layout L = Layout::make(C, N, kLanes);
         const int f = L.first(lane), cnt = L.count(lane);
         const bool is_short = lane < L.n_short;
         // per-slot LDS byte offsets of em[., tok[j-1]]
@@ -203,7 +208,7 @@ struct Forward {
 
         if (MODE == 1) {
             if (lane == 0) tr[0] = col0;
-            for (int j = lane + 1; j <= N; j += kWave) tr[j] = -INFINITY;
+            for (int j = lane + 1; j <= N; j += kLanes) tr[j] = -INFINITY;
         }
 
         const int nch = (T + kChunk - 1) / kChunk;
@@ -216,7 +221,7 @@ struct Forward {
             __syncthreads();
             if (q + 1 < nch) stage_rows<VS>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
                                           lds + ((q + 1) & 1) * kChunk * VS);
-            if (MODE == 0 && lane < rows) q0[q * kChunk + lane] = exp_cr(buf[lane * VS]);
+            if (MODE == 0 && lane < rows) q0[q * kChunk + lane] = exp_cr(buf[lane * VS]);  // wave 0
             const char* bb = reinterpret_cast<const char*>(buf);
             int r = 0;
             // ---- unrolled groups of kUnroll steps with immediate LDS row offsets
@@ -228,7 +233,7 @@ struct Forward {
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
                     step(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best,
-                         best_t, nan_t, tr);
+                         best_t, nan_t, tr, xch);
                     ++t;
                 }
             }
@@ -238,29 +243,37 @@ struct Forward {
                 const char* ga[C];
 #pragma unroll
                 for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best, best_t, nan_t, tr);
+                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best, best_t, nan_t, tr,
+                     xch);
                 ++t;
             }
             if (MODE == 0) {
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
-                    bits[((int64_t)q * C + k) * kWave + lane] = (sh == 0) ? w[k] : (w[k] << sh);
+                    bits[((int64_t)q * C + k) * kLanes + lane] = (sh == 0) ? w[k] : (w[k] << sh);
                     w[k] = 0u;
                 }
             }
         }
         if (MODE == 0) {
-            const int bt = __builtin_amdgcn_readlane(best_t, gN);
-            const int nt = __builtin_amdgcn_readlane(nan_t, gN);
-            *t_start_out = nt > 0 ? nt : bt;
+            const int bt = __builtin_amdgcn_readlane(best_t, gN & (kWave - 1));
+            const int nt = __builtin_amdgcn_readlane(nan_t, gN & (kWave - 1));
+            if (W == 1) {
+                *t_start_out = nt > 0 ? nt : bt;
+            } else {  // the owner wave of column N broadcasts through LDS
+                if (uniform(lane >> 6) == (gN >> 6) && (lane & (kWave - 1)) == 0) *tsb = nt > 0 ? nt : bt;
+                __syncthreads();
+                *t_start_out = *tsb;
+            }
         }
     }
 
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 cellvec<C>& cur, unsigned (&w)[C], double& acc, float& col0,
                                                 int t, int T, int N, int lane, bool is_short, int f, int cnt,
-                                                float& best, int& best_t, int& nan_t, float* __restrict__ tr) {
+                                                float& best, int& best_t, int& nan_t, float* __restrict__ tr,
+                                                float* xch) {
         const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
         const float e0 = *reinterpret_cast<const float*>(gb + ro);
         float et[C];
@@ -268,7 +281,15 @@ struct Forward {
         for (int k = 0; k < C; ++k) et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
         // last cell of the lane to the left (short lanes end at slot C-2)
         const float src = (C > 1 && is_short) ? cur[C > 1 ? C - 2 : 0] : cur[C - 1];
-        const float left = dpp_shr1(col0, src);
+        float in0 = col0;  // what lane 0 of this wave sees on its left
+        if constexpr (W > 1) {
+            const int wv = lane >> 6;
+            float* slot = xch + (t & 1) * W;
+            if ((lane & (kWave - 1)) == kWave - 1) slot[wv] = src;
+            __syncthreads();
+            if (wv > 0) in0 = slot[wv - 1];
+        }
+        const float left = dpp_shr1(in0, src);
 #pragma unroll
         for (int k = C - 1; k >= 0; --k) {
             const float s = cur[k] + eb;
@@ -285,8 +306,7 @@ struct Forward {
             best = gt ? v : best;
             nan_t = (v != v && nan_t == 0) ? t + 1 : nan_t;
         } else {
-            const int64_t W = (int64_t)N + 1;
-            float* row = tr + (int64_t)(t + 1) * W;
+            float* row = tr + (int64_t)(t + 1) * ((int64_t)N + 1);
             if (lane == 0) row[0] = col0;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
@@ -307,7 +327,7 @@ __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bit
     if (jj < 1) return 0u;
     int g, k;
     lay.locate(jj - 1, g, k);
-    return bits[((int64_t)b * lay.C + k) * kWave + g];
+    return bits[((int64_t)b * lay.C + k) * lay.lanes + g];
 }
 
 __device__ bool walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start,
@@ -345,7 +365,7 @@ __device__ bool walk(const unsigned* __restrict__ bits, const Layout& lay, int N
 __device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* __restrict__ tok, int N, int t_start,
                              const float* __restrict__ q0, const int32_t* __restrict__ start, int32_t* __restrict__ seg_end,
                              double* __restrict__ seg_score) {
-    for (int k = lane_id(); k < N; k += kWave) {
+    for (int k = (int)threadIdx.x; k < N; k += (int)blockDim.x) {
         const int s = start[k];
         const int e = (k + 1 < N) ? start[k + 1] : t_start;
         int tk = tok[k];
@@ -363,21 +383,29 @@ __device__ __forceinline__ void block_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// Cells-per-lane buckets (one kernel instantiation each).
-#define WX_CELL_BUCKETS(X) X(1) X(2) X(4) X(6) X(8) X(12) X(16) X(24) X(32)
+// (cells per lane C, waves per segment W) buckets, one kernel instantiation each.
+// Single-wave buckets cover N <= 2048; longer transcripts use W waves that exchange the
+// boundary cell through LDS once per step.
+#define WX_BUCKETS(X) \
+    X(1, 1) X(2, 1) X(4, 1) X(6, 1) X(8, 1) X(12, 1) X(16, 1) X(24, 1) X(32, 1) X(16, 4) X(16, 8) X(32, 8)
 
-__host__ __device__ __forceinline__ int bucket_cells(int N) {
+__host__ __device__ __forceinline__ int bucket_id(int N) {  // = C * 64 + W
     const int need = (N + kWave - 1) / kWave;
-    if (need <= 1) return 1;
-    if (need <= 2) return 2;
-    if (need <= 4) return 4;
-    if (need <= 6) return 6;
-    if (need <= 8) return 8;
-    if (need <= 12) return 12;
-    if (need <= 16) return 16;
-    if (need <= 24) return 24;
-    return 32;
+    if (need <= 1) return 1 * 64 + 1;
+    if (need <= 2) return 2 * 64 + 1;
+    if (need <= 4) return 4 * 64 + 1;
+    if (need <= 6) return 6 * 64 + 1;
+    if (need <= 8) return 8 * 64 + 1;
+    if (need <= 12) return 12 * 64 + 1;
+    if (need <= 16) return 16 * 64 + 1;
+    if (need <= 24) return 24 * 64 + 1;
+    if (need <= 32) return 32 * 64 + 1;
+    if (need <= 64) return 16 * 64 + 4;
+    if (need <= 128) return 16 * 64 + 8;
+    return 32 * 64 + 8;
 }
+
+__host__ __device__ __forceinline__ int bucket_cells_total(int id) { return (id / 64) * kWave * (id % 64); }
 
 struct AlignArgs {
     const float* em;
@@ -397,13 +425,15 @@ struct AlignArgs {
     float* q0;       // workspace: sum_T floats
 };
 
-template <int C, int VS>
-__global__ __launch_bounds__(kWave) void align_dp_kernel(AlignArgs a) {
+template <int C, int VS, int W>
+__global__ __launch_bounds__(kWave * W) void align_dp_kernel(AlignArgs a) {
     __shared__ float lds[2 * kChunk * VS];
+    __shared__ float xch[2 * W];
+    __shared__ int tsb[2];
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
-    if (bucket_cells(d.N) != C) return;  // another instantiation owns this segment
-    const int lane = lane_id();
+    if (bucket_id(d.N) != C * 64 + W) return;  // another instantiation owns this segment
+    const int lane = (int)threadIdx.x;
     if (d.N <= 0 || d.T <= 0) {
         if (lane == 0) {
             a.t_start[seg] = 0;
@@ -415,14 +445,20 @@ __global__ __launch_bounds__(kWave) void align_dp_kernel(AlignArgs a) {
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
     int ts = 0;
-    Forward<C, VS, 0>::run(d, E, a.V, a.tok, bits, q0, nullptr, &ts, lds);
+    Forward<C, VS, 0, W>::run(d, E, a.V, a.tok, bits, q0, nullptr, &ts, lds, xch, tsb);
     if (lane == 0) a.t_start[seg] = ts;
+    wait_vm();
     block_fence();
     int32_t* start = a.seg_start + d.tok0;
-    const bool ok = walk(bits, Layout::make(C, d.N), d.N, ts, start);
+    if (lane < kWave) {  // wave 0 walks
+        const bool okw = walk(bits, Layout::make(C, d.N, kWave * W), d.N, ts, start);
+        if (lane == 0) tsb[1] = okw ? 1 : 0;
+    }
+    wait_vm();
+    block_fence();
+    const bool ok = tsb[1] != 0;
     if (lane == 0) a.status[seg] = ok ? 0 : 1;
     if (!ok) return;
-    block_fence();
     merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
 }
 
@@ -437,20 +473,21 @@ struct TrellisArgs {
     const int64_t* tr_off;
 };
 
-template <int C, int VS>
-__global__ __launch_bounds__(kWave) void trellis_kernel(TrellisArgs a) {
+template <int C, int VS, int W>
+__global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
     __shared__ float lds[2 * kChunk * VS];
+    __shared__ float xch[2 * W];
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
-    if (bucket_cells(d.N) != C) return;
+    if (bucket_id(d.N) != C * 64 + W) return;
     float* tr = a.tr + a.tr_off[seg];
-    const int lane = lane_id();
+    const int lane = (int)threadIdx.x;
     if (d.N == 0) {  // the whole single column is +inf (alignment.py:369-370 with num_tokens = 0)
-        for (int t = lane; t <= d.T; t += kWave) tr[t] = INFINITY;
+        for (int t = lane; t <= d.T; t += kWave * W) tr[t] = INFINITY;
         return;
     }
     const float* E = a.em + d.row0 * a.V;
-    Forward<C, VS, 1>::run(d, E, a.V, a.tok, nullptr, nullptr, tr, nullptr, lds);
+    Forward<C, VS, 1, W>::run(d, E, a.V, a.tok, nullptr, nullptr, tr, nullptr, lds, xch, nullptr);
 }
 
 // ------------------------------------------------------------------------------------
@@ -565,6 +602,7 @@ __global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
         lay.C = cpl;
         lay.G = kWave;
         lay.n_short = 0;
+        lay.lanes = kWave;
         const bool ok = walk(bits, lay, N, ts, start);
         if (threadIdx.x == 0) ok_sh = ok ? 1 : 0;
     }
@@ -845,10 +883,10 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // bitmap: per segment (floor(row0/32) + seg) block offsets, 64 * C_stride dwords per block
 size_t bitmap_bytes(int32_t S, int64_t sum_T, int64_t max_N, int* stride_cells) {
-    const int C = bucket_cells((int)std::max<int64_t>(max_N, 1));
-    if (stride_cells) *stride_cells = kWave * C;
+    const int cells = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
+    if (stride_cells) *stride_cells = cells;
     const int64_t blocks = sum_T / kChunk + S + 1;
-    return align_up((size_t)blocks * (size_t)kWave * (size_t)C * 4u, 256);
+    return align_up((size_t)blocks * (size_t)cells * 4u, 256);
 }
 
 }  // namespace
@@ -862,7 +900,7 @@ const char* wx_strerror(int code) {
         case WX_OK: return "ok";
         case WX_E_INVALID: return "invalid argument";
         case WX_E_VOCAB: return "vocabulary size outside [1, 64]";
-        case WX_E_TOO_LONG: return "segment has more than 2048 tokens";
+        case WX_E_TOO_LONG: return "segment has more than 16384 tokens";
         case WX_E_WORKSPACE: return "workspace too small";
         case WX_E_LAUNCH: return "kernel launch failed";
         default: return hipGetErrorString((hipError_t)code);
@@ -892,16 +930,16 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t
     a.bits = reinterpret_cast<unsigned*>(workspace);
     a.q0 = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + bm);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int lo = bucket_cells((int)std::max<int64_t>(min_N, 1)), hi = bucket_cells((int)std::max<int64_t>(max_N, 1));
-    const dim3 grid(S), block(kWave);
-    // N == 0 segments belong to the C=1 bucket (bucket_cells(0) == 1) and are handled there.
-    const int lo_eff = (min_N == 0) ? 1 : lo;
-#define WX_LAUNCH_ALIGN(CC)                                                                       \
-    if (CC >= lo_eff && CC <= hi) {                                                               \
-        if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32>), grid, block, 0, st, a);       \
-        else hipLaunchKernelGGL((align_dp_kernel<CC, 64>), grid, block, 0, st, a);               \
+    // buckets are ordered by capacity; N == 0 segments belong to the first one
+    const int lo = bucket_cells_total(bucket_id((int)std::max<int64_t>(min_N, 1)));
+    const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
+    const dim3 grid(S);
+#define WX_LAUNCH_ALIGN(CC, WW)                                                                          \
+    if (CC * kWave * WW >= lo && CC * kWave * WW <= hi) {                                              \
+        if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, st, a); \
+        else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, st, a);         \
     }
-    WX_CELL_BUCKETS(WX_LAUNCH_ALIGN)
+    WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
     return launch_status();
 }
@@ -918,14 +956,14 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
     a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id;
     a.tr = trellis; a.tr_off = tr_off;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int hi = bucket_cells((int)std::max<int64_t>(max_N, 1));
-    const dim3 grid(S), block(kWave);
-#define WX_LAUNCH_TR(CC)                                                                          \
-    if (CC <= hi) {                                                                               \
-        if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32>), grid, block, 0, st, a);        \
-        else hipLaunchKernelGGL((trellis_kernel<CC, 64>), grid, block, 0, st, a);                \
+    const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
+    const dim3 grid(S);
+#define WX_LAUNCH_TR(CC, WW)                                                                            \
+    if (CC * kWave * WW <= hi) {                                                                      \
+        if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, st, a); \
+        else hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, st, a);         \
     }
-    WX_CELL_BUCKETS(WX_LAUNCH_TR)
+    WX_BUCKETS(WX_LAUNCH_TR)
 #undef WX_LAUNCH_TR
     return launch_status();
 }
