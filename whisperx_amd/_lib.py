@@ -102,8 +102,21 @@ def _stream(device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _h2d(x, dtype, device):
+    """Host list/array -> device tensor through pinned memory.  An async copy from a
+    temporary *pageable* tensor is unsafe here (the staging buffer can be recycled before
+    the copy runs); the caching host allocator keeps a pinned block alive until its copy
+    has completed on the stream."""
+    h = torch.as_tensor(x, dtype=dtype)
+    if h.dim() == 0:
+        h = h.reshape(1)
+    if torch.cuda.is_available():
+        h = h.pin_memory()
+    return h.to(device, non_blocking=True)
+
+
 def _dev_i64(x, device):
-    return torch.as_tensor(x, dtype=torch.int64).to(device, non_blocking=True)
+    return _h2d(x, torch.int64, device)
 
 
 class Workspace:
@@ -155,8 +168,8 @@ class Batch:
             em = torch.empty((0, self.V), dtype=torch.float32, device=device)
         self.em = em.contiguous()
         flat = [int(x) for t in tokens for x in t]
-        self.tok = torch.tensor(flat if flat else [0], dtype=torch.int32).to(device, non_blocking=True)
-        self.blank = torch.tensor([int(b) for b in blank_ids] or [0], dtype=torch.int32).to(device, non_blocking=True)
+        self.tok = _h2d(flat if flat else [0], torch.int32, device)
+        self.blank = _h2d([int(b) for b in blank_ids] or [0], torch.int32, device)
         self.em_off_d = _dev_i64(self.em_off, device)
         self.tok_off_d = _dev_i64(self.tok_off, device)
         self.min_N = min(self.Ns) if self.Ns else 0
@@ -257,8 +270,8 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
     for n in F:
         r_off.append(r_off[-1] + n + 1)
     ys = torch.cat([torch.as_tensor(s, dtype=torch.float32).reshape(-1) for s in scores_list]) if F else torch.zeros(1)
-    ys = ys.to(dev)
-    g = torch.tensor(sw_geometry, dtype=torch.float64).reshape(-1, 3).to(dev)
+    ys = _h2d(ys, torch.float32, dev)
+    g = _h2d(torch.tensor(sw_geometry, dtype=torch.float64).reshape(-1, 3), torch.float64, dev)
     st0, stp, dur = g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].contiguous()
     rs = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
     re = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
