@@ -212,9 +212,10 @@ def trellis(b: Batch):
     for T, N in zip(b.Ts, b.Ns):
         offs.append(offs[-1] + (T + 1) * (N + 1))
     out = torch.empty(max(offs[-1], 1), dtype=torch.float32, device=dev)
+    offs_d = _dev_i64(offs, dev)  # keep referenced until the launch is enqueued
     with torch.cuda.device(dev):
         _check(lib.wx_trellis(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank),
-                              b.S, b.max_N, _ptr(out), _ptr(_dev_i64(offs, dev)), _stream(dev)))
+                              b.S, b.max_N, _ptr(out), _ptr(offs_d), _stream(dev)))
     return out, offs
 
 
@@ -230,8 +231,9 @@ def backtrack(b: Batch, tr_flat: torch.Tensor, tr_offs):
     ts = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
     wsb = lib.wx_backtrack_workspace_bytes(b.S, b.sum_T, b.max_N)
     ws = _ws.get(dev, wsb)
+    tr_off_d = _dev_i64(tr_offs, dev)
     with torch.cuda.device(dev):
-        _check(lib.wx_backtrack(_ptr(tr_flat), _ptr(_dev_i64(tr_offs, dev)), _ptr(b.em), _ptr(b.em_off_d), b.V,
+        _check(lib.wx_backtrack(_ptr(tr_flat), _ptr(tr_off_d), _ptr(b.em), _ptr(b.em_off_d), b.V,
                                 _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S, b.max_N, b.sum_T,
                                 _ptr(pt), _ptr(pm), _ptr(pp), _ptr(plen), _ptr(ts), _ptr(ws), wsb, _stream(dev)))
     return pt, pm, pp, plen, ts
@@ -276,10 +278,11 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
     rs = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
     re = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
     cnt = torch.empty(max(len(F), 1), dtype=torch.int64, device=dev)
+    f_off_d, r_off_d = _dev_i64(f_off, dev), _dev_i64(r_off, dev)  # referenced until enqueued
     with torch.cuda.device(dev):
-        _check(lib.wx_binarize(_ptr(ys), _ptr(_dev_i64(f_off, dev)), len(F), _ptr(st0), _ptr(stp), _ptr(dur),
+        _check(lib.wx_binarize(_ptr(ys), _ptr(f_off_d), len(F), _ptr(st0), _ptr(stp), _ptr(dur),
                                float(np.float32(onset)), float(np.float32(offset)), float(max_duration),
-                               float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(_dev_i64(r_off, dev)),
+                               float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(r_off_d),
                                _ptr(cnt), _stream(dev)))
     cnt_h = cnt.cpu().numpy()
     rs_h, re_h = rs.cpu().numpy(), re.cpu().numpy()
