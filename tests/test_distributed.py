@@ -1,0 +1,83 @@
+"""Per-file sharding and the vocabulary broadcast on a world_size-2 gloo group (CPU)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from whisperx_amd.distributed import (_decode_dictionary, _encode_dictionary, align_corpus,
+                                      broadcast_dictionary, gather_results, shard_files)
+
+
+def test_shard_files_lpt_balanced_and_complete():
+    durs = [60, 1, 45, 30, 30, 12, 5, 59, 2, 33]
+    for world in (1, 2, 4, 8):
+        shards = shard_files(durs, world)
+        flat = sorted(i for s in shards for i in s)
+        assert flat == list(range(len(durs)))
+        loads = [sum(durs[i] for i in s) for s in shards]
+        assert max(loads) - min(loads) <= max(durs)
+    assert shard_files(durs, 2) == shard_files(list(durs), 2)  # deterministic
+
+
+def test_shard_files_config4_corpus():
+    import numpy as np
+
+    rng = np.random.default_rng(4)
+    d = np.exp(rng.uniform(np.log(60), np.log(3600), 40))
+    d = d / d.sum() * 36000.0  # 10 h
+    shards = shard_files(d.tolist(), 8)
+    loads = [d[s].sum() for s in shards]
+    assert max(loads) / (36000.0 / 8) < 1.25
+
+
+def test_dictionary_codec_roundtrip():
+    d = {"<pad>": 0, "<s>": 1, "|": 4, "e": 5, "'": 27, "ü": 40, "日": 41}
+    assert _decode_dictionary(_encode_dictionary(d)) == d
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vocab = {"<pad>": 0, "|": 4, "e": 5, "t": 6, "ä": 33} if rank == 0 else None
+        got = broadcast_dictionary(vocab, device=None)
+        durs = [30.0, 10.0, 25.0, 5.0, 60.0]
+        res = align_corpus([f"f{i}" for i in range(5)], lambda f: {"file": f, "rank": rank}, durs)
+        q.put((rank, got, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_and_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs.sort(key=lambda x: x[0])
+    for rank, got, res in outs:
+        assert got == {"<pad>": 0, "|": 4, "e": 5, "t": 6, "ä": 33}
+    merged = outs[0][2]
+    assert outs[1][2] is None
+    assert sorted(merged) == [0, 1, 2, 3, 4]
+    shards = shard_files([30.0, 10.0, 25.0, 5.0, 60.0], 2)
+    for r in (0, 1):
+        for i in shards[r]:
+            assert merged[i] == {"file": f"f{i}", "rank": r}

@@ -203,6 +203,33 @@ def align_dp(b: Batch):
     return seg_start, seg_end, seg_score, t_start, status
 
 
+class AlignPlan:
+    """Preallocated outputs + workspace for repeated wx_align_dp calls on one batch (the
+    bench's timed step, and any caller that re-aligns a resident batch)."""
+
+    def __init__(self, b: Batch):
+        self.lib = load()
+        _validate(b)
+        self.b = b
+        dev = b.device
+        nt = max(b.tok_off[-1], 1)
+        self.seg_start = torch.empty(nt, dtype=torch.int32, device=dev)
+        self.seg_end = torch.empty(nt, dtype=torch.int32, device=dev)
+        self.seg_score = torch.empty(nt, dtype=torch.float64, device=dev)
+        self.t_start = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+        self.status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
+        self.wsb = self.lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
+        self.ws = torch.empty(max(self.wsb, 1), dtype=torch.uint8, device=dev)
+        self.args = (_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S,
+                     b.min_N, b.max_N, b.sum_T, _ptr(self.seg_start), _ptr(self.seg_end), _ptr(self.seg_score),
+                     _ptr(self.t_start), _ptr(self.status), _ptr(self.ws), self.wsb)
+
+    def run(self, stream=None):
+        st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.b.device).cuda_stream)
+        _check(self.lib.wx_align_dp(*self.args, st))
+        return self.seg_start, self.seg_end, self.seg_score, self.t_start, self.status
+
+
 def trellis(b: Batch):
     """Materialised trellises (CSR): returns (flat tensor, offsets list)."""
     lib = load()

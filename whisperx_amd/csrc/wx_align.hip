@@ -33,6 +33,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <mutex>
+
 #include "../../include/wx_align.h"
 
 #define WX_VERSION "0.1.0"
@@ -881,6 +884,73 @@ int launch_status() {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Kernels of different (C, W) buckets are independent: a batch that spans several buckets
+// forks them onto a small per-device pool of non-blocking streams and joins back onto the
+// caller's stream with events, so they run concurrently (a latency-bound batch then costs
+// the slowest bucket, not their sum).  Created once per device; enqueue is serialised by
+// a mutex so concurrent callers cannot interleave fork/join events.
+struct ForkPool {
+    static constexpr int kMax = 12;
+    hipStream_t s[kMax];
+    hipEvent_t fork;
+    hipEvent_t join[kMax];
+    std::mutex mu;
+};
+
+ForkPool* fork_pool() {
+    static std::mutex mu;
+    static ForkPool* pools[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!pools[dev]) {
+        ForkPool* p = new ForkPool;
+        bool ok = hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < ForkPool::kMax; ++i) {
+            ok = hipStreamCreateWithFlags(&p->s[i], hipStreamNonBlocking) == hipSuccess &&
+                 hipEventCreateWithFlags(&p->join[i], hipEventDisableTiming) == hipSuccess;
+        }
+        if (!ok) return nullptr;
+        pools[dev] = p;
+    }
+    return pools[dev];
+}
+
+// Run launch(i, stream) for i in [0, n): on the caller's stream when n == 1, otherwise
+// forked over the pool and joined back onto `st`.
+template <class F>
+int fork_join(hipStream_t st, int n, F&& launch) {
+    if (n <= 0) return WX_OK;
+    if (n == 1) {
+        launch(0, st);
+        return launch_status();
+    }
+    ForkPool* p = fork_pool();
+    if (!p || n > ForkPool::kMax) {  // serial fallback on the caller's stream
+        for (int i = 0; i < n; ++i) launch(i, st);
+        return launch_status();
+    }
+    std::lock_guard<std::mutex> g(p->mu);
+    hipError_t e = hipEventRecord(p->fork, st);
+    for (int i = 0; i < n && e == hipSuccess; ++i) {
+        e = hipStreamWaitEvent(p->s[i], p->fork, 0);
+        if (e != hipSuccess) break;
+        launch(i, p->s[i]);
+        e = hipEventRecord(p->join[i], p->s[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, p->join[i], 0);
+    }
+    const int rc = launch_status();
+    return e != hipSuccess ? (int)e : rc;
+}
+
+// bucket ids in launch order, ids = C*64 + W
+constexpr int kBucketIds[] = {
+#define WX_ID(CC, WW) CC * 64 + WW,
+    WX_BUCKETS(WX_ID)
+#undef WX_ID
+};
+constexpr int kNumBuckets = sizeof(kBucketIds) / sizeof(int);
+
 // bitmap: per segment (floor(row0/32) + seg) block offsets, 64 * C_stride dwords per block
 size_t bitmap_bytes(int32_t S, int64_t sum_T, int64_t max_N, int* stride_cells) {
     const int cells = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
@@ -933,15 +1003,21 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t
     // buckets are ordered by capacity; N == 0 segments belong to the first one
     const int lo = bucket_cells_total(bucket_id((int)std::max<int64_t>(min_N, 1)));
     const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
-    const dim3 grid(S);
-#define WX_LAUNCH_ALIGN(CC, WW)                                                                          \
-    if (CC * kWave * WW >= lo && CC * kWave * WW <= hi) {                                              \
-        if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, st, a); \
-        else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, st, a);         \
+    int ids[kNumBuckets], n = 0;
+    for (int i = 0; i < kNumBuckets; ++i) {
+        const int cells = bucket_cells_total(kBucketIds[i]);
+        if (cells >= lo && cells <= hi) ids[n++] = kBucketIds[i];
     }
-    WX_BUCKETS(WX_LAUNCH_ALIGN)
+    const dim3 grid(S);
+    return fork_join(st, n, [&](int i, hipStream_t s) {
+#define WX_LAUNCH_ALIGN(CC, WW)                                                                          \
+        if (ids[i] == CC * 64 + WW) {                                                                  \
+            if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
+            else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a);         \
+        }
+        WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
-    return launch_status();
+    });
 }
 
 int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
@@ -957,15 +1033,19 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
     a.tr = trellis; a.tr_off = tr_off;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
+    int ids[kNumBuckets], n = 0;
+    for (int i = 0; i < kNumBuckets; ++i)
+        if (bucket_cells_total(kBucketIds[i]) <= hi) ids[n++] = kBucketIds[i];
     const dim3 grid(S);
+    return fork_join(st, n, [&](int i, hipStream_t s) {
 #define WX_LAUNCH_TR(CC, WW)                                                                            \
-    if (CC * kWave * WW <= hi) {                                                                      \
-        if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, st, a); \
-        else hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, st, a);         \
-    }
-    WX_BUCKETS(WX_LAUNCH_TR)
+        if (ids[i] == CC * 64 + WW) {                                                                 \
+            if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
+            else hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a);         \
+        }
+        WX_BUCKETS(WX_LAUNCH_TR)
 #undef WX_LAUNCH_TR
-    return launch_status();
+    });
 }
 
 size_t wx_backtrack_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {

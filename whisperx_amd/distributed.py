@@ -1,0 +1,103 @@
+"""Per-file data parallelism across the GPUs of a node.
+
+One process per GPU (torchrun; LOCAL_RANK -> device).  Alignment/VAD work has no
+cross-segment dependence, so files are partitioned across ranks and every rank aligns
+its own files with no collective on the data path.  The only collectives:
+
+  * broadcast_dictionary: the alignment model's character vocabulary from rank 0
+    (a few hundred bytes; backend "nccl" = RCCL over xGMI on ROCm, "gloo" on CPU);
+  * gather_results (optional): per-file result dicts to rank 0 (gather_object).
+
+shard_files balances mixed-length corpora (BASELINE config 4: 40 files of 1-60 min)
+longest-processing-time first: files sorted by duration (descending, index as tie
+break), each assigned to the currently least-loaded rank (lowest rank on ties).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def shard_files(durations: Sequence[float], world_size: int) -> List[List[int]]:
+    """LPT assignment of file indices to ranks; deterministic on every rank."""
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    order = sorted(range(len(durations)), key=lambda i: (-float(durations[i]), i))
+    load = [0.0] * world_size
+    shards: List[List[int]] = [[] for _ in range(world_size)]
+    for i in order:
+        r = min(range(world_size), key=lambda k: (load[k], k))
+        shards[r].append(i)
+        load[r] += float(durations[i])
+    for s in shards:
+        s.sort()
+    return shards
+
+
+def _encode_dictionary(d: Dict[str, int]) -> torch.Tensor:
+    """[n_entries, 2 + L] int32: (id, n_codepoints, codepoints..., 0-padded)."""
+    items = sorted(d.items(), key=lambda kv: (kv[1], kv[0]))
+    L = max((len(k) for k, _ in items), default=0)
+    t = torch.zeros((len(items), 2 + L), dtype=torch.int32)
+    for r, (k, v) in enumerate(items):
+        t[r, 0] = int(v)
+        t[r, 1] = len(k)
+        for c, ch in enumerate(k):
+            t[r, 2 + c] = ord(ch)
+    return t
+
+
+def _decode_dictionary(t: torch.Tensor) -> Dict[str, int]:
+    out = {}
+    for row in t.tolist():
+        n = row[1]
+        out["".join(chr(c) for c in row[2:2 + n])] = row[0]
+    return out
+
+
+def broadcast_dictionary(dictionary: Optional[Dict[str, int]], device=None, src: int = 0) -> Dict[str, int]:
+    """Broadcast rank `src`'s {char: id} vocabulary to every rank (two broadcasts: shape,
+    then the packed table).  Device tensors for RCCL, CPU tensors for gloo."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return dict(dictionary)
+    backend = dist.get_backend()
+    dev = torch.device(device) if (device is not None and backend != "gloo") else torch.device("cpu")
+    if dist.get_rank() == src:
+        packed = _encode_dictionary(dictionary)
+        shape = torch.tensor(list(packed.shape), dtype=torch.int64)
+    else:
+        packed = None
+        shape = torch.zeros(2, dtype=torch.int64)
+    shape = shape.to(dev)
+    dist.broadcast(shape, src)
+    if packed is None:
+        packed = torch.zeros(tuple(int(x) for x in shape.tolist()), dtype=torch.int32)
+    packed = packed.to(dev)
+    dist.broadcast(packed, src)
+    return _decode_dictionary(packed.cpu())
+
+
+def gather_results(local: Dict[int, dict], dst: int = 0) -> Optional[Dict[int, dict]]:
+    """Collect {file_index: result} from every rank on `dst` (None elsewhere)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return dict(local)
+    bucket = [None] * dist.get_world_size() if dist.get_rank() == dst else None
+    dist.gather_object(local, bucket, dst=dst)
+    if dist.get_rank() != dst:
+        return None
+    merged: Dict[int, dict] = {}
+    for part in bucket:
+        merged.update(part)
+    return dict(sorted(merged.items()))
+
+
+def align_corpus(files, align_fn, durations: Sequence[float], gather: bool = True):
+    """Run align_fn(file) for this rank's share of `files`; optionally gather to rank 0.
+    `align_fn` is the per-file pipeline (e.g. VAD merge_chunks -> ASR segments -> align)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    mine = shard_files(durations, world)[rank]
+    local = {i: align_fn(files[i]) for i in mine}
+    return gather_results(local) if gather else local
