@@ -51,13 +51,15 @@ __device__ __forceinline__ float nan_max(float a, float b) {
     return __builtin_elementwise_maximum(a, b);
 }
 
-// w <- 2w + (c > s): strict compare (false when unordered), shifted into a column word.
+// w <- 2w + (c > s): strict compare (false when unordered) into a private SGPR pair,
+// then add-with-carry shifts it into the lane's 32-step column word.  Not volatile and no
+// VCC: the cells of a step are free to interleave.
 __device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
     unsigned r;
-    asm("v_cmp_gt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %3, %3, vcc"
-        : "=v"(r)
-        : "v"(c), "v"(s), "v"(w)
-        : "vcc");
+    unsigned long long m;
+    asm("v_cmp_gt_f32_e64 %1, %2, %3\n\tv_addc_co_u32_e64 %0, %1, %4, %4, %1"
+        : "=v"(r), "=&s"(m)
+        : "v"(c), "v"(s), "v"(w));
     return r;
 }
 
@@ -69,6 +71,17 @@ __device__ __forceinline__ float dpp_shr1(float old_lane0, float v) {
     return __builtin_bit_cast(
         float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old_lane0), __builtin_bit_cast(int, v),
                                            0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+}
+
+// ring[lane] = v (v, lane wave-uniform).  gfx950 reads one SGPR per VALU op over the
+// constant bus, so the lane select goes through M0 (saved and restored in the statement;
+// the s_nop covers the M0 write -> v_writelane lane-select hazard).
+__device__ __forceinline__ float write_lane(float ring, float v, int lane) {
+    unsigned keep;
+    asm("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
+        : "+v"(ring), "=&s"(keep)
+        : "s"(v), "s"(lane));
+    return ring;
 }
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
@@ -102,13 +115,31 @@ __device__ __forceinline__ SegDesc load_desc(const int64_t* em_off, const int64_
 // Stage emission rows [r0, r0+nrows) of a segment into LDS buffer `dst` (row stride VS
 // floats) with global_load_lds: one dword per lane, one instruction per row, lanes >= V
 // masked.  Asynchronous: the caller waits vmcnt before reading.
+// LDS byte address of a __shared__ pointer (for M0).
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+// One global_load_lds_dword: lane l's dword lands at LDS m0 + 4*l.  Issued from inline asm
+// so that hipcc's waitcnt pass does not see it (it would otherwise drain vmcnt before every
+// ds_read, serialising the prefetch); callers wait vmcnt(0) themselves before reading.
+__device__ __forceinline__ void glds_dword(const float* gsrc, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
 template <int VS>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
     const int lane = (int)threadIdx.x;  // wave 0 stages for the whole workgroup
+    if (uniform(lane >> 6) != 0) return;
+    const unsigned base = (unsigned)uniform((int)lds_addr(dst));
     if (lane < V) {
         for (int r = 0; r < nrows; ++r) {
             const float* src = E + (int64_t)(r0 + r) * V + lane;
-            __builtin_amdgcn_global_load_lds(src, dst + r * VS, 4, 0, 0);
+            glds_dword(src, base + (unsigned)(r * VS * 4));
         }
     }
 }
@@ -205,9 +236,12 @@ struct Forward {
 
         double acc = 0.0;
         float col0 = col0_value(0, 0.0, T, N);
-        // argmax over column N (row 0 is -inf): first strict max; the first NaN wins outright
+        // argmax over column N (row 0 is -inf): first strict max; the first NaN wins outright.
+        // Per step the owner's value is copied into `ring` (lane r = step r of the chunk);
+        // each chunk is reduced once (running state uniform across the wave).
         float best = -INFINITY;
         int best_t = 0, nan_t = 0;
+        float ring = 0.f;
 
         if (MODE == 1) {
             if (lane == 0) tr[0] = col0;
@@ -235,8 +269,8 @@ struct Forward {
                 for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
-                    step(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best,
-                         best_t, nan_t, tr, xch);
+                    step(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, ring,
+                         r + u, gN, tr, xch);
                     ++t;
                 }
             }
@@ -246,11 +280,11 @@ struct Forward {
                 const char* ga[C];
 #pragma unroll
                 for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, best, best_t, nan_t, tr,
-                     xch);
+                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, ring, r, gN, tr, xch);
                 ++t;
             }
             if (MODE == 0) {
+                reduce_chunk(ring, rows, q * kChunk + 1, best, best_t, nan_t);
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
@@ -260,23 +294,48 @@ struct Forward {
             }
         }
         if (MODE == 0) {
-            const int bt = __builtin_amdgcn_readlane(best_t, gN & (kWave - 1));
-            const int nt = __builtin_amdgcn_readlane(nan_t, gN & (kWave - 1));
+            const int ts = nan_t > 0 ? nan_t : best_t;  // uniform within each wave
             if (W == 1) {
-                *t_start_out = nt > 0 ? nt : bt;
+                *t_start_out = ts;
             } else {  // the owner wave of column N broadcasts through LDS
-                if (uniform(lane >> 6) == (gN >> 6) && (lane & (kWave - 1)) == 0) *tsb = nt > 0 ? nt : bt;
+                if (uniform(lane >> 6) == (gN >> 6) && (lane & (kWave - 1)) == 0) *tsb = ts;
                 __syncthreads();
                 *t_start_out = *tsb;
             }
         }
     }
 
+    // Fold one chunk of column-N values (ring lane i = row t0 + i) into the running argmax
+    // with torch.argmax semantics (first maximum; the first NaN wins and is final).
+    __device__ __forceinline__ static void reduce_chunk(float ring, int rows, int t0, float& best, int& best_t,
+                                                        int& nan_t) {
+        const int l = lane_id();
+        const bool valid = l < rows;
+        const bool isn = valid && (ring != ring);
+        const unsigned long long nm = __ballot(isn);
+        if (nan_t == 0 && nm) nan_t = t0 + (__ffsll((long long)nm) - 1);
+        float v = valid ? ring : -INFINITY;
+        int idx = valid ? l : kChunk;
+#pragma unroll
+        for (int off = 1; off < kChunk; off <<= 1) {  // (max, first index), NaN rows excluded
+            const float v2 = __shfl_xor(v, off);
+            const int i2 = __shfl_xor(idx, off);
+            const bool take = (v2 > v) || (v2 == v && i2 < idx) || (v != v && v2 == v2);
+            v = take ? v2 : v;
+            idx = take ? i2 : idx;
+        }
+        v = __shfl(v, 0);
+        idx = __shfl(idx, 0);
+        if (v == v && v > best && idx < rows) {
+            best = v;
+            best_t = t0 + idx;
+        }
+    }
+
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 cellvec<C>& cur, unsigned (&w)[C], double& acc, float& col0,
                                                 int t, int T, int N, int lane, bool is_short, int f, int cnt,
-                                                float& best, int& best_t, int& nan_t, float* __restrict__ tr,
-                                                float* xch) {
+                                                float& ring, int r, int gN, float* __restrict__ tr, float* xch) {
         const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
         const float e0 = *reinterpret_cast<const float*>(gb + ro);
         float et[C];
@@ -303,11 +362,9 @@ struct Forward {
         acc += (double)e0;
         col0 = col0_value(t + 1, acc, T, N);
         if (MODE == 0) {
-            const float v = cur[C - 1];
-            const bool gt = v > best;
-            best_t = gt ? t + 1 : best_t;
-            best = gt ? v : best;
-            nan_t = (v != v && nan_t == 0) ? t + 1 : nan_t;
+            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cur[C - 1]),
+                                                                               gN & (kWave - 1)));
+            ring = write_lane(ring, v, r);
         } else {
             float* row = tr + (int64_t)(t + 1) * ((int64_t)N + 1);
             if (lane == 0) row[0] = col0;
