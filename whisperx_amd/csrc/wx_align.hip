@@ -73,17 +73,6 @@ __device__ __forceinline__ float dpp_shr1(float old_lane0, float v) {
                                            0x138 /* wave_shr:1 */, 0xF, 0xF, false));
 }
 
-// ring[lane] = v (v, lane wave-uniform).  gfx950 reads one SGPR per VALU op over the
-// constant bus, so the lane select goes through M0 (saved and restored in the statement;
-// the s_nop covers the M0 write -> v_writelane lane-select hazard).
-__device__ __forceinline__ float write_lane(float ring, float v, int lane) {
-    unsigned keep;
-    asm("s_mov_b32 %1, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tv_writelane_b32 %0, %2, m0\n\ts_mov_b32 m0, %1"
-        : "+v"(ring), "=&s"(keep)
-        : "s"(v), "s"(lane));
-    return ring;
-}
-
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -364,7 +353,7 @@ struct Forward {
         if (MODE == 0) {
             const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cur[C - 1]),
                                                                                gN & (kWave - 1)));
-            ring = write_lane(ring, v, r);
+            ring = (lane_id() == r) ? v : ring;  // v_cmp_eq + v_cndmask; hazards handled by hipcc
         } else {
             float* row = tr + (int64_t)(t + 1) * ((int64_t)N + 1);
             if (lane == 0) row[0] = col0;
