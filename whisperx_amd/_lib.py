@@ -16,7 +16,7 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwxalign.so")
+LIB_PATH = os.environ.get("WX_LIB_PATH") or os.path.join(_HERE, "libwxalign.so")
 SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 

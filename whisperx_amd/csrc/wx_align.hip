@@ -51,15 +51,21 @@ __device__ __forceinline__ float nan_max(float a, float b) {
     return __builtin_elementwise_maximum(a, b);
 }
 
-// w <- 2w + (c > s): strict compare (false when unordered) into a private SGPR pair,
-// then add-with-carry shifts it into the lane's 32-step column word.  Not volatile and no
-// VCC: the cells of a step are free to interleave.
+// w <- 2w + (c > s): strict compare (false when unordered), shifted into the lane's
+// 32-step column word with an add-with-carry.
 __device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
     unsigned r;
+#ifdef WX_SHIFT_SGPR
     unsigned long long m;
     asm("v_cmp_gt_f32_e64 %1, %2, %3\n\tv_addc_co_u32_e64 %0, %1, %4, %4, %1"
         : "=v"(r), "=&s"(m)
         : "v"(c), "v"(s), "v"(w));
+#else
+    asm("v_cmp_gt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %3, %3, vcc"
+        : "=v"(r)
+        : "v"(c), "v"(s), "v"(w)
+        : "vcc");
+#endif
     return r;
 }
 
@@ -128,7 +134,11 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, i
     if (lane < V) {
         for (int r = 0; r < nrows; ++r) {
             const float* src = E + (int64_t)(r0 + r) * V + lane;
+#ifdef WX_GLDS_BUILTIN
+            __builtin_amdgcn_global_load_lds(src, dst + r * VS, 4, 0, 0);
+#else
             glds_dword(src, base + (unsigned)(r * VS * 4));
+#endif
         }
     }
 }
@@ -274,6 +284,9 @@ struct Forward {
             }
             if (MODE == 0) {
                 reduce_chunk(ring, rows, q * kChunk + 1, best, best_t, nan_t);
+#ifdef WX_DEBUG_RING
+                if (lane < rows) q0[q * kChunk + lane] = ring;
+#endif
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
@@ -351,7 +364,12 @@ struct Forward {
         acc += (double)e0;
         col0 = col0_value(t + 1, acc, T, N);
         if (MODE == 0) {
-            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cur[C - 1]),
+            // column N = slot C-1 of lane gN.  The empty asm pins the operand: without it
+            // hipcc (ROCm 7.2) folded this readlane into the DPP-source select above and read
+            // slot C-2 (caught by the golden tests).
+            float vN = cur[C - 1];
+            asm volatile("" : "+v"(vN));
+            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vN),
                                                                                gN & (kWave - 1)));
             ring = (lane_id() == r) ? v : ring;  // v_cmp_eq + v_cndmask; hazards handled by hipcc
         } else {
