@@ -45,6 +45,7 @@ namespace wx {
 constexpr int kWave = 64;
 constexpr int kChunk = 32;  // emission rows per LDS buffer == bits per column word
 constexpr int kUnroll = 8;  // time steps per unrolled group
+constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
 __device__ __forceinline__ float nan_max(float a, float b) {
     // IEEE-754-2019 maximum (NaN-propagating): torch.maximum for non-zero-sign cases.
@@ -235,6 +236,7 @@ struct Forward {
 
         double acc = 0.0;
         float col0 = col0_value(0, 0.0, T, N);
+        const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
         // argmax over column N (row 0 is -inf): first strict max; the first NaN wins outright.
         // Per step the owner's value is copied into `ring` (lane r = step r of the chunk);
         // each chunk is reduced once (running state uniform across the wave).
@@ -266,11 +268,20 @@ struct Forward {
                 const char* ga[C];
 #pragma unroll
                 for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
+                if (t + kUnroll < inf_from) {  // every row of the group has a finite column 0
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    step(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, ring,
-                         r + u, gN, tr, xch);
-                    ++t;
+                    for (int u = 0; u < kUnroll; ++u) {
+                        step<true>(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f,
+                                   cnt, ring, r + u, gN, N, tr, xch);
+                        ++t;
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u) {
+                        step<false>(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f,
+                                    cnt, ring, r + u, gN, N, tr, xch);
+                        ++t;
+                    }
                 }
             }
             // ---- remainder steps (last partial group)
@@ -279,7 +290,8 @@ struct Forward {
                 const char* ga[C];
 #pragma unroll
                 for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-                step(gb, ga, 0, boff, cur, w, acc, col0, t, T, N, lane, is_short, f, cnt, ring, r, gN, tr, xch);
+                step<false>(gb, ga, 0, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f, cnt, ring, r, gN, N,
+                            tr, xch);
                 ++t;
             }
             if (MODE == 0) {
@@ -334,10 +346,12 @@ struct Forward {
         }
     }
 
+    template <bool FINITE_COL0>
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 cellvec<C>& cur, unsigned (&w)[C], double& acc, float& col0,
-                                                int t, int T, int N, int lane, bool is_short, int f, int cnt,
-                                                float& ring, int r, int gN, float* __restrict__ tr, float* xch) {
+                                                int t, int inf_from, int lane, bool is_short, int f, int cnt,
+                                                float& ring, int r, int gN, int N, float* __restrict__ tr,
+                                                float* xch) {
         const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
         const float e0 = *reinterpret_cast<const float*>(gb + ro);
         float et[C];
@@ -362,13 +376,13 @@ struct Forward {
             cur[k] = nan_max(s, c);
         }
         acc += (double)e0;
-        col0 = col0_value(t + 1, acc, T, N);
+        col0 = (FINITE_COL0 || t + 1 < inf_from) ? (float)acc : INFINITY;
         if (MODE == 0) {
             // column N = slot C-1 of lane gN.  The empty asm pins the operand: without it
             // hipcc (ROCm 7.2) folded this readlane into the DPP-source select above and read
             // slot C-2 (caught by the golden tests).
             float vN = cur[C - 1];
-            asm volatile("" : "+v"(vN));
+            asm("" : "+v"(vN));  // opaque, but not a scheduling barrier
             const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vN),
                                                                                gN & (kWave - 1)));
             ring = (lane_id() == r) ? v : ring;  // v_cmp_eq + v_cndmask; hazards handled by hipcc
@@ -397,34 +411,85 @@ __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bit
     return bits[((int64_t)b * lay.C + k) * lay.lanes + g];
 }
 
-__device__ bool walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start,
-                     int32_t* __restrict__ start) {
-    if (t_start <= 0 || N <= 0) return false;
+// Walk one 32-step block (decision indices 32b+s_hi .. 32b) from window offset d.
+// Purely scalar: the only vector instruction is the v_readlane of the column word.
+// Returns the block's change mask (bit 31-s = the path moved onto a new token at 32b+s).
+template <bool FULL>
+__device__ __forceinline__ unsigned walk_block(unsigned win, int& d, int s_hi) {
+    unsigned cm = 0u;
+    if (FULL) {
+#pragma unroll
+        for (int s = 31; s >= 0; --s) {
+            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, d);
+            const unsigned bit = (word >> (31 - s)) & 1u;
+            cm |= bit << (31 - s);
+            d += (int)bit;
+        }
+    } else {
+        for (int s = s_hi; s >= 0; --s) {
+            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, d);
+            const unsigned bit = (word >> (31 - s)) & 1u;
+            cm |= bit << (31 - s);
+            d = uniform(d + (int)bit);
+        }
+    }
+    return cm;
+}
+
+// The backtrack walk (alignment.py:395-421) over the decision bitmap: from (t_start, N),
+// step back one frame at a time and move to the previous token where the decision bit is
+// set.  Once j reaches 0 the window reads cell 0 (all zero), so blocks run to completion
+// without an early-exit test.  Per block only the change mask is kept (cmask[b]);
+// start frames are compacted from it afterwards.  Returns the lowest block touched, or -1
+// where the reference returns None.
+__device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask) {
+    if (t_start <= 0 || N <= 0) return -1;
     int j = N;
-    int u = t_start - 1;  // decision index = t - 1
-    int b = u >> 5;
+    int b = (t_start - 1) >> 5;
     int A = j;
     unsigned win = load_window(bits, lay, b, A);
     int An = A;
     unsigned nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
-    const bool writer = lane_id() == 0;
+    int d = 0;
+    unsigned cm = walk_block<false>(win, d, (t_start - 1) & 31);
     while (true) {
-        const int lo = b << 5;
-        while (u >= lo) {
-            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, A - j);
-            if ((word >> (31 - (u & 31))) & 1u) {
-                if (writer) start[j - 1] = u;
-                --j;
-                if (j == 0) return true;
-            }
-            --u;
-        }
-        if (u < 0) return false;
+        cmask[b] = cm;
+        j = uniform(A - d);
+        if (j <= 0) return b;
+        if (b == 0) return -1;
         --b;
         win = nxt;
         A = An;
         An = j;
         nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
+        d = A - j;
+        cm = walk_block<true>(win, d, 31);
+    }
+}
+
+// start[k] = k-th change frame in increasing time: a popcount prefix over the change masks
+// of blocks [b_lo, b_hi] (wave 0).
+__device__ void compact_starts(const unsigned* cmask, int b_lo, int b_hi, int32_t* __restrict__ start) {
+    const int lane = lane_id();
+    int base = 0;
+    for (int b0 = b_lo; b0 <= b_hi; b0 += kWave) {
+        const int b = b0 + lane;
+        const unsigned m = (b <= b_hi) ? cmask[b] : 0u;
+        const int c = __popc(m);
+        int incl = c;  // inclusive wave scan of popcounts
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        int k = base + incl - c;
+        unsigned mm = m;
+        while (mm) {  // bit 31 = lowest frame of the block
+            const int p = 31 - __clz(mm);
+            start[k++] = b * kChunk + (31 - p);
+            mm &= ~(1u << p);
+        }
+        base += __shfl(incl, kWave - 1);
     }
 }
 
@@ -442,6 +507,14 @@ __device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* 
         seg_end[k] = e;
         seg_score[k] = sum / (double)(e - s);
     }
+}
+
+// Order one wave's own global/LDS writes before its later reads by other lanes (no
+// barrier: safe inside wave-divergent regions of multi-wave workgroups).
+__device__ __forceinline__ void wave_fence() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 __device__ __forceinline__ void block_fence() {
@@ -490,11 +563,13 @@ struct AlignArgs {
     unsigned* bits;  // workspace: bitmap region
     int bits_stride_cells;  // 64 * Cstride dwords per block
     float* q0;       // workspace: sum_T floats
+    unsigned* cmask; // workspace: walk change masks, (floor(row0/32) + seg) words per segment
 };
 
 template <int C, int VS, int W>
 __global__ __launch_bounds__(kWave * W) void align_dp_kernel(AlignArgs a) {
     __shared__ float lds[2 * kChunk * VS];
+    __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ float xch[2 * W];
     __shared__ int tsb[2];
     const int seg = blockIdx.x;
@@ -517,9 +592,14 @@ __global__ __launch_bounds__(kWave * W) void align_dp_kernel(AlignArgs a) {
     wait_vm();
     block_fence();
     int32_t* start = a.seg_start + d.tok0;
-    if (lane < kWave) {  // wave 0 walks
-        const bool okw = walk(bits, Layout::make(C, d.N, kWave * W), d.N, ts, start);
-        if (lane == 0) tsb[1] = okw ? 1 : 0;
+    if (lane < kWave) {  // wave 0 walks, then compacts the change masks into start frames
+        unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
+        const int b_lo = walk(bits, Layout::make(C, d.N, kWave * W), d.N, ts, cmask);
+        if (b_lo >= 0) {
+            wave_fence();
+            compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
+        }
+        if (lane == 0) tsb[1] = b_lo >= 0 ? 1 : 0;
     }
     wait_vm();
     block_fence();
@@ -578,6 +658,7 @@ struct BacktrackArgs {
     unsigned* bits;
     int bits_stride_cells;
     int32_t* start;  // workspace: per-token start frames (CSR by tok_off)
+    unsigned* cmask; // workspace: walk change masks
 };
 
 __global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
@@ -670,11 +751,17 @@ __global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
         lay.G = kWave;
         lay.n_short = 0;
         lay.lanes = kWave;
-        const bool ok = walk(bits, lay, N, ts, start);
+        unsigned* cmask = a.cmask + ((d.row0 >> 5) + seg);
+        const int b_lo = walk(bits, lay, N, ts, cmask);
+        if (b_lo >= 0) {
+            wave_fence();
+            compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
+        }
+        const bool ok = b_lo >= 0;
         if (threadIdx.x == 0) ok_sh = ok ? 1 : 0;
     }
-    __threadfence_block();
-    __syncthreads();
+    wait_vm();
+    block_fence();
     const bool ok = ok_sh != 0;
     if (threadIdx.x == 0) a.path_len[seg] = ok ? (ts - start[0]) : -1;
     if (!ok) return;
@@ -1041,8 +1128,10 @@ const char* wx_strerror(int code) {
     }
 }
 
+size_t cmask_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T / kChunk + S + 1) * 4u, 256); }
+
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
-    return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256);
+    return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T);
 }
 
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
@@ -1063,6 +1152,8 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t
     const size_t bm = bitmap_bytes(S, sum_T, max_N, &a.bits_stride_cells);
     a.bits = reinterpret_cast<unsigned*>(workspace);
     a.q0 = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + bm);
+    a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
+                                          align_up((size_t)(sum_T + 1) * 4u, 256));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // buckets are ordered by capacity; N == 0 segments belong to the first one
     const int lo = bucket_cells_total(bucket_id((int)std::max<int64_t>(min_N, 1)));
@@ -1116,7 +1207,8 @@ size_t wx_backtrack_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
     const int64_t cpl = std::max<int64_t>(1, (max_N + kWave - 1) / kWave);
     const int64_t blocks = sum_T / kChunk + S + 1;
     // bitmap + per-token start frames (sum of N <= S * max_N)
-    return align_up((size_t)blocks * kWave * (size_t)cpl * 4u, 256) + align_up((size_t)(S * max_N + 1) * 4u, 256);
+    return align_up((size_t)blocks * kWave * (size_t)cpl * 4u, 256) + align_up((size_t)(S * max_N + 1) * 4u, 256) +
+           cmask_bytes(S, sum_T);
 }
 
 int wx_backtrack(const float* trellis, const int64_t* tr_off, const float* em, const int64_t* em_off, int32_t V,
@@ -1140,6 +1232,8 @@ int wx_backtrack(const float* trellis, const int64_t* tr_off, const float* em, c
     const size_t bm = align_up((size_t)blocks * kWave * (size_t)cpl * 4u, 256);
     a.bits = reinterpret_cast<unsigned*>(workspace);
     a.start = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(workspace) + bm);
+    a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
+                                          align_up((size_t)(S * max_N + 1) * 4u, 256));
     hipLaunchKernelGGL(backtrack_kernel, dim3(S), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
     return launch_status();
 }
