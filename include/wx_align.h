@@ -50,7 +50,7 @@ enum {
 };
 
 #define WX_MAX_VOCAB 64      /* emission columns held in LDS per row */
-#define WX_MAX_TOKENS 16384  /* tokens per segment (8 waves x 64 lanes x 32 cells) */
+#define WX_MAX_TOKENS 16000  /* tokens per segment (8 waves x 64 lanes x 32 cells, less halos) */
 
 const char* wx_version(void);
 const char* wx_strerror(int code);
@@ -97,6 +97,21 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
                 int32_t* seg_start, int32_t* seg_end, double* seg_score,
                 int32_t* t_start, int32_t* status,
                 void* workspace, size_t workspace_bytes, void* stream);
+
+/* wx_align_dp with an explicit launch shape (results are identical in every mode):
+ *   WX_MODE_AUTO        latency shape for batches of <= 256 segments, else throughput;
+ *   WX_MODE_THROUGHPUT  one wave per segment up to 2048 tokens (most segments in flight);
+ *   WX_MODE_LATENCY     each segment's columns spread over up to 8 waves (shortest time
+ *                       per segment when the batch cannot fill the GPU).
+ * wx_align_dp == wx_align_dp_mode(..., WX_MODE_AUTO) unless the environment variable
+ * WX_ALIGN_MODE=0/1 forces a shape (benchmarking). */
+enum { WX_MODE_AUTO = -1, WX_MODE_THROUGHPUT = 0, WX_MODE_LATENCY = 1 };
+int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V,
+                     const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
+                     int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T,
+                     int32_t* seg_start, int32_t* seg_end, double* seg_score,
+                     int32_t* t_start, int32_t* status,
+                     void* workspace, size_t workspace_bytes, int32_t mode, void* stream);
 
 /* Binarize.__call__ (vad.py:118-180) for n_files score columns (CSR by f_off) with
  * pyannote sliding-window geometry per file (frame i is centred at

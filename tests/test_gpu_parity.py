@@ -89,11 +89,11 @@ def _random_cases(rng, n, T_range, N_range, V, quant=None, blank=None):
     return cases
 
 
-def _check_vs_oracle(cases, tag):
+def _check_vs_oracle(cases, tag, mode=-1):
     from whisperx_amd import _lib
 
     b = _batch(cases)
-    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b))
+    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b, mode=mode))
     mism = 0
     for s, c in enumerate(cases):
         ok, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
@@ -107,8 +107,9 @@ def _check_vs_oracle(cases, tag):
     return mism
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("V", [29, 32, 40, 64])
-def test_align_dp_random_mixed_buckets_vs_oracle(V):
+def test_align_dp_random_mixed_buckets_vs_oracle(V, mode):
     rng = np.random.default_rng(V)
     cases = []
     # every cells-per-lane bucket: N in (1..64], (64..128], ... (1536..2048]
@@ -117,21 +118,52 @@ def test_align_dp_random_mixed_buckets_vs_oracle(V):
         cases += _random_cases(rng, 2, (max(hi + 8, 40), hi + 700), (lo, hi), V)
     cases += _random_cases(rng, 6, (20, 300), (1, 60), V, quant=16)  # exact ties
     cases += _random_cases(rng, 4, (5, 40), (20, 60), V)  # N > T: backtrack fails
-    _check_vs_oracle(cases, f"V{V}")
+    _check_vs_oracle(cases, f"V{V} mode {mode}", mode)
+
+
+def _capacity(C, W):
+    """Tokens a (C cells/lane, W waves) bucket holds: waves >= 1 give ceil(32/C) lanes to the
+    chunk halo (wx_align.hip, Geometry)."""
+    return C * (64 + (W - 1) * (64 - ((32 + C - 1) // C if W > 1 else 0)))
+
+
+THROUGHPUT_BUCKETS = [(1, 1), (2, 1), (4, 1), (6, 1), (8, 1), (12, 1), (16, 1), (24, 1), (32, 1), (16, 4), (16, 8)]
+LATENCY_BUCKETS = [(1, 1), (1, 3), (1, 7), (2, 3), (2, 7), (4, 7), (8, 7), (16, 8)]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_align_dp_bucket_capacity_edges(mode):
+    """N at every bucket capacity and one past it (column N in the last lane of the last wave,
+    halo lanes holding column N's left neighbours), in both launch shapes, V=32 (16-byte
+    staging) and V=29 (row staging)."""
+    rng = np.random.default_rng(100 + mode)
+    Ns = set()
+    for C, W in (THROUGHPUT_BUCKETS if mode == 0 else LATENCY_BUCKETS):
+        cap = _capacity(C, W)
+        if cap <= 4001 or (mode == 0 and cap <= 8000):
+            Ns.update({cap, cap + 1})
+    for V in (32, 29):
+        cases = []
+        for N in sorted(Ns):
+            T = N + int(rng.integers(2, 70))
+            cases += _random_cases(rng, 1, (T, T + 1), (N, N + 1), V, blank=0)
+        _check_vs_oracle(cases, f"edges V{V} mode {mode}", mode)
 
 
 def test_align_dp_config2_batch_vs_oracle():
     """BASELINE config 2: 64 x 30 s segments (T=1499, V=32, N~U[300,500])."""
     rng = np.random.default_rng(2)
     cases = _random_cases(rng, 64, (1499, 1500), (300, 501), 32, blank=0)
-    _check_vs_oracle(cases, "cfg2")
+    for mode in (0, 1):
+        _check_vs_oracle(cases, f"cfg2 mode {mode}", mode)
 
 
 def test_align_dp_config5_long_form_vs_oracle():
     """BASELINE config 5: DE large-xlsr-shaped, T=2999, V=40, N~900."""
     rng = np.random.default_rng(5)
     cases = _random_cases(rng, 8, (2999, 3000), (850, 951), 40, blank=0)
-    _check_vs_oracle(cases, "cfg5")
+    for mode in (0, 1):
+        _check_vs_oracle(cases, f"cfg5 mode {mode}", mode)
 
 
 def test_align_dp_deterministic_and_order_independent():

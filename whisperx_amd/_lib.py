@@ -21,7 +21,7 @@ SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 MAX_VOCAB = 64
-MAX_TOKENS = 16384
+MAX_TOKENS = 16000
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -42,6 +42,8 @@ SIGNATURES = {
     "wx_align_dp_workspace_bytes": (_sz, [_i32, _i64, _i64]),
     "wx_align_dp": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "wx_align_dp_mode": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
+                                        _vp, _vp, _vp, _vp, _vp, _vp, _sz, _i32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
 }
@@ -183,8 +185,12 @@ def _validate(b: Batch):
         raise WXError(f"a segment has {b.max_N} tokens; the kernel supports up to {MAX_TOKENS}")
 
 
-def align_dp(b: Batch):
-    """Fused DP: returns device tensors (seg_start, seg_end, seg_score, t_start, status)."""
+MODE_AUTO, MODE_THROUGHPUT, MODE_LATENCY = -1, 0, 1
+
+
+def align_dp(b: Batch, mode: int = MODE_AUTO):
+    """Fused DP: returns device tensors (seg_start, seg_end, seg_score, t_start, status).
+    `mode` picks the launch shape (WX_MODE_*); results are identical in every mode."""
     lib = load()
     _validate(b)
     dev = b.device
@@ -197,9 +203,10 @@ def align_dp(b: Batch):
     wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
     ws = _ws.get(dev, wsb)
     with torch.cuda.device(dev):
-        _check(lib.wx_align_dp(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank),
-                               b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end), _ptr(seg_score),
-                               _ptr(t_start), _ptr(status), _ptr(ws), wsb, _stream(dev)))
+        _check(lib.wx_align_dp_mode(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d),
+                                    _ptr(b.blank), b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end),
+                                    _ptr(seg_score), _ptr(t_start), _ptr(status), _ptr(ws), wsb, int(mode),
+                                    _stream(dev)))
     return seg_start, seg_end, seg_score, t_start, status
 
 
@@ -207,10 +214,11 @@ class AlignPlan:
     """Preallocated outputs + workspace for repeated wx_align_dp calls on one batch (the
     bench's timed step, and any caller that re-aligns a resident batch)."""
 
-    def __init__(self, b: Batch):
+    def __init__(self, b: Batch, mode: int = MODE_AUTO):
         self.lib = load()
         _validate(b)
         self.b = b
+        self.mode = int(mode)
         dev = b.device
         nt = max(b.tok_off[-1], 1)
         self.seg_start = torch.empty(nt, dtype=torch.int32, device=dev)
@@ -226,7 +234,7 @@ class AlignPlan:
 
     def run(self, stream=None):
         st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.b.device).cuda_stream)
-        _check(self.lib.wx_align_dp(*self.args, st))
+        _check(self.lib.wx_align_dp_mode(*self.args, self.mode, st))
         return self.seg_start, self.seg_end, self.seg_score, self.t_start, self.status
 
 

@@ -33,6 +33,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <mutex>
 
@@ -108,37 +110,61 @@ __device__ __forceinline__ SegDesc load_desc(const int64_t* em_off, const int64_
     return d;
 }
 
-// Stage emission rows [r0, r0+nrows) of a segment into LDS buffer `dst` (row stride VS
-// floats) with global_load_lds: one dword per lane, one instruction per row, lanes >= V
-// masked.  Asynchronous: the caller waits vmcnt before reading.
 // LDS byte address of a __shared__ pointer (for M0).
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
-// One global_load_lds_dword: lane l's dword lands at LDS m0 + 4*l.  Issued from inline asm
-// so that hipcc's waitcnt pass does not see it (it would otherwise drain vmcnt before every
+// Wave-uniform 64-bit pointer (SGPR pair).
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return (const float*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// LDS-DMA loads (global_load_lds), saddr form: wave-uniform base + 32-bit lane offset
+// (inline-asm 64-bit VGPR operands are not guaranteed the even alignment gfx950 requires).
+// Lane l's dword (or 16 bytes) lands at LDS m0 + 4*l (16*l).  Issued from inline asm so
+// that hipcc's waitcnt pass does not see them (it would otherwise drain vmcnt before every
 // ds_read, serialising the prefetch); callers wait vmcnt(0) themselves before reading.
-__device__ __forceinline__ void glds_dword(const float* gsrc, unsigned lds_dst) {
+__device__ __forceinline__ void glds_dword(const float* sbase, unsigned voff, unsigned lds_dst) {
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
+                 : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds_dst)
+                 : "memory");
+}
+__device__ __forceinline__ void glds_dwordx4(const float* sbase, unsigned voff, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds_dst)
                  : "memory");
 }
 
-template <int VS>
-__device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
-    const int lane = (int)threadIdx.x;  // wave 0 stages for the whole workgroup
-    if (uniform(lane >> 6) != 0) return;
+// Stage emission rows [r0, r0+nrows) of a segment into LDS buffer `dst` (row stride VS
+// floats).  Every wave of the workgroup issues its share.  When V == VS == 32 and the
+// rows are 16-byte aligned (`x4`), a chunk is one contiguous 4 KB block in both places:
+// one 16-byte-per-lane instruction moves 8 rows.  Otherwise one dword per lane per row,
+// lanes >= V masked.  Asynchronous: every wave waits vmcnt(0) before the chunk barrier.
+template <int VS, int W, bool ONE_WAVE = false>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst,
+                                           bool x4) {
+    const int wv = ONE_WAVE ? 0 : uniform((int)threadIdx.x >> 6);
+    const int l = lane_id();
     const unsigned base = (unsigned)uniform((int)lds_addr(dst));
-    if (lane < V) {
-        for (int r = 0; r < nrows; ++r) {
-            const float* src = E + (int64_t)(r0 + r) * V + lane;
+    if (VS == 32 && x4) {
+        for (int i = wv; i * 8 < nrows; i += W) {
+            if (i * 8 + (l >> 3) < nrows)
+                glds_dwordx4(E + (int64_t)(r0 + i * 8) * 32, (unsigned)l * 16u, base + (unsigned)(i * 1024));
+        }
+    } else if (l < V) {
+        for (int r = wv; r < nrows; r += W) {
 #ifdef WX_GLDS_BUILTIN
-            __builtin_amdgcn_global_load_lds(src, dst + r * VS, 4, 0, 0);
+            __builtin_amdgcn_global_load_lds(E + (int64_t)(r0 + r) * V + l, dst + r * VS, 4, 0, 0);
 #else
-            glds_dword(src, base + (unsigned)(r * VS * 4));
+            glds_dword(E + (int64_t)(r0 + r) * V, (unsigned)l * 4u, base + (unsigned)(r * VS * 4));
 #endif
         }
     }
@@ -179,42 +205,135 @@ struct Layout {
         return g < n_short ? g * (C - 1) + 1 : n_short * (C - 1) + (g - n_short) * C + 1;
     }
     __device__ __forceinline__ int count(int g) const { return g < n_short ? C - 1 : (g < G ? C : 0); }
-    // (lane, slot) of 0-based cell c
+    // (lane, slot) of 0-based cell c; CC = C when known at compile time (0: runtime C)
+    template <int CC = 0>
     __device__ __forceinline__ void locate(int c, int& g, int& k) const {
-        const int cs = n_short * (C - 1);
+        const int Cc = CC > 0 ? CC : C;
+        const int cs = n_short * (Cc - 1);
         if (c < cs) {
-            g = c / (C - 1);
-            k = c - g * (C - 1);
+            g = Cc > 1 ? c / (Cc - 1) : 0;
+            k = c - g * (Cc - 1);
         } else {
             const int c2 = c - cs;
-            g = n_short + c2 / C;
-            k = c2 - (g - n_short) * C;
+            g = n_short + c2 / Cc;
+            k = c2 - (g - n_short) * Cc;
         }
     }
 };
 
 // ------------------------------------------------------------------------------------
+#ifdef WX_PHASE_TIMING
+// Debug build only: per-segment s_memtime at kernel entry / forward end / walk end / exit,
+// plus s_memrealtime at entry and exit (100 MHz) to convert cycles to time.
+__device__ unsigned long long wx_phase[8192 * 6];
+// per (segment, wave): cycles in steps / barrier waits / other chunk work
+__device__ unsigned long long wx_loop[8192 * 16 * 3];
+#define WX_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define WX_STAMP(i) \
+    if (threadIdx.x == 0 && seg < 8192) wx_phase[seg * 6 + (i)] = __builtin_amdgcn_s_memtime()
+#define WX_STAMP_RT(i) \
+    if (threadIdx.x == 0 && seg < 8192) wx_phase[seg * 6 + (i)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define WX_STAMP(i)
+#define WX_STAMP_RT(i)
+#define WX_T(v)
+#endif
+
 // The trellis forward pass shared by the fused and the materialising kernels.
-//   MODE 0: fused — per-cell 32-step decision words -> bits, argmax of column N, q0 row.
+//   MODE 0: fused — per-cell 32-step decision words -> bits, column N history -> cn.
 //   MODE 1: materialise — write every trellis row (get_trellis).
-template <int C, int VS, int MODE, int W>
+//
+// W > 1 waves split the columns of one segment with a chunk halo instead of a per-step
+// exchange: wave w >= 1 spends its first HL = ceil(32/C) lanes re-computing the last HL
+// lanes of wave w-1 (>= 32 cells).  At each chunk start (row 32q) those cells are copied
+// from wave w-1 through LDS; during the chunk's 32 steps the wrong value that enters at
+// the halo's left edge moves right by one cell per step, so it never reaches the wave's
+// own cells (cell j at row t depends only on cells j-s..j at row t-s).  The waves meet
+// once per chunk at the barrier that also publishes the staged emission rows.  Halo lanes
+// compute bit-identical copies (same operands, same order) and only the owning lane
+// writes decisions / trellis values.
+//
+// H (helper): one more wave per workgroup stages the emission rows two chunks ahead and
+// computes column 0 (the fp64 cumsum, +inf rows) and q0 = exp(em[t,0]) one chunk ahead, so
+// the column-1 wave reads column 0 from LDS instead of running the fp64 chain per step.
+template <int C, int W>
+struct Geometry {
+    static constexpr int HL = W > 1 ? (32 + C - 1) / C : 0;  // halo lanes per wave >= 1
+    static constexpr int kUseful = kWave + (W - 1) * (kWave - HL);  // useful lanes
+    static constexpr int kCapacity = C * kUseful;                   // max N
+    // useful lane index of (wave, lane); for a halo lane, the lane it mirrors
+    __host__ __device__ static constexpr int lane_of(int wv, int l) {
+        return wv == 0 ? l : kWave + (wv - 1) * (kWave - HL) + l - HL;
+    }
+    // (wave, lane) owning useful lane g
+    __device__ static void owner(int g, int& wv, int& l) {
+        if (g < kWave || W == 1) {
+            wv = 0;
+            l = g;
+        } else {
+            wv = 1 + (g - kWave) / (kWave - HL);
+            l = HL + (g - kWave) % (kWave - HL);
+        }
+    }
+};
+
+template <int C, int VS, int MODE, int W, bool H>
 struct Forward {
     static constexpr int kRowBytes = VS * 4;
-    static constexpr int kLanes = kWave * W;
+    static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves)
+    static constexpr int kBufs = H ? 3 : 2;   // emission chunk buffers in LDS
+    using Geo = Geometry<C, W>;
+    static_assert(!(H && MODE == 1), "the materialising kernel computes column 0 in wave 0");
 
-    __device__ static void run(const SegDesc& d, const float* __restrict__ E, int V,
-                               const int32_t* __restrict__ tok,
-                               unsigned* __restrict__ bits,   // MODE 0: segment's bitmap
-                               float* __restrict__ q0,         // MODE 0: exp(em[t,0]) per row
-                               float* __restrict__ tr,         // MODE 1: trellis
-                               int* t_start_out, float* lds /* 2 * kChunk * VS */,
-                               float* xch /* 2 * W: cross-wave neighbour exchange */,
-                               int* tsb /* t_start broadcast */) {
-        const int lane = (int)threadIdx.x;  // lane within the workgroup (W waves)
+    // Per-lane state of the forward pass.
+    struct State {
+        cellvec<C> cur;
+        unsigned w[C];
+        double acc;   // W == 1 / !H: column-0 cumsum (fp64)
+        float col0;   // tr[t][0] for the current step (column-1 wave)
+        int t;
+    };
+
+    // All waves of the workgroup call run(); with H, wave W is the helper.
+    __device__ __forceinline__ static void run(const SegDesc& d, const float* __restrict__ E, int V,
+                                               const int32_t* __restrict__ tok,
+                                               unsigned* __restrict__ bits,  // MODE 0: segment's bitmap
+                                               float* __restrict__ q0,        // MODE 0: exp(em[t,0]) per row
+                                               float* __restrict__ cn,        // MODE 0: column N of rows 1..T
+                                               float* __restrict__ tr,        // MODE 1: trellis
+                                               float* lds /* kBufs * kChunk * VS */,
+                                               float* c0b /* H: 2 * kChunk column-0 values */,
+                                               float* xh /* 2 * W * 64: chunk halo copies */, bool x4) {
+        const int wv = uniform((int)threadIdx.x >> 6);
         const int T = d.T, N = d.N;
+        const int nch = (T + kChunk - 1) / kChunk;
+        if (H && wv == W) {
+            helper(d, E, V, lds, c0b, nch, x4);
+            return;
+        }
+        const int l = lane_id();
         const Layout L = Layout::make(C, N, kLanes);
-        const int f = L.first(lane), cnt = L.count(lane);
-        const bool is_short = lane < L.n_short;
+        if (MODE == 1) {
+            if (threadIdx.x == 0) tr[0] = col0_value(0, 0.0, T, N);
+            for (int j = (int)threadIdx.x + 1; j <= N; j += kLanes) tr[j] = -INFINITY;
+        }
+        if (W > 1 && wv > 0 && Geo::lane_of(wv, Geo::HL) >= L.G) {
+            // no column of this wave exists: keep the barrier count (and, without a helper,
+            // this wave's share of the staging)
+            if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4);
+            for (int q = 0; q < nch; ++q) {
+                wait_vm();
+                __syncthreads();
+                if (!H && q + 1 < nch)
+                    stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
+                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4);
+            }
+            return;
+        }
+        const int g = Geo::lane_of(wv, l);  // useful lane this lane computes
+        const bool halo = wv > 0 && l < Geo::HL;
+        const int f = L.first(g), cnt = L.count(g);
+        const bool is_short = g < L.n_short;
         // per-slot LDS byte offsets of em[., tok[j-1]]
         int toff[C];
 #pragma unroll
@@ -225,213 +344,317 @@ struct Forward {
             toff[k] = tk * 4;
         }
         const int boff = d.blank * 4;
-        const int gN = uniform(L.G - 1);  // column N = slot C-1 of lane G-1
+        // column N = slot C-1 of useful lane G-1
+        int own_w, own_l;
+        Geo::owner(L.G - 1, own_w, own_l);
+        const bool owner = uniform(own_w) == wv && l == own_l;
 
-        cellvec<C> cur;
+        State st;
 #pragma unroll
-        for (int k = 0; k < C; ++k) cur[k] = -INFINITY;  // row 0, columns 1..N
-        unsigned w[C];
+        for (int k = 0; k < C; ++k) st.cur[k] = -INFINITY;  // row 0, columns 1..N
 #pragma unroll
-        for (int k = 0; k < C; ++k) w[k] = 0u;
-
-        double acc = 0.0;
-        float col0 = col0_value(0, 0.0, T, N);
+        for (int k = 0; k < C; ++k) st.w[k] = 0u;
+        st.acc = 0.0;
+        st.col0 = col0_value(0, 0.0, T, N);
+        st.t = 0;
         const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
-        // argmax over column N (row 0 is -inf): first strict max; the first NaN wins outright.
-        // Per step the owner's value is copied into `ring` (lane r = step r of the chunk);
-        // each chunk is reduced once (running state uniform across the wave).
-        float best = -INFINITY;
-        int best_t = 0, nan_t = 0;
-        float ring = 0.f;
 
-        if (MODE == 1) {
-            if (lane == 0) tr[0] = col0;
-            for (int j = lane + 1; j <= N; j += kLanes) tr[j] = -INFINITY;
-        }
-
-        const int nch = (T + kChunk - 1) / kChunk;
-        if (nch > 0) stage_rows<VS>(E, V, 0, min(kChunk, T), lds);
-        int t = 0;
+        if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4);
+#ifdef WX_PHASE_TIMING
+        unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0;
+#endif
         for (int q = 0; q < nch; ++q) {
-            float* buf = lds + (q & 1) * kChunk * VS;
+            WX_T(c0);
+            float* buf = lds + (q % kBufs) * kChunk * VS;
             const int rows = min(kChunk, T - q * kChunk);
+            float* xq = xh + (q & 1) * W * kWave;
+            if (W > 1 && q > 0 && wv < W - 1 && l >= kWave - Geo::HL) {  // publish this chunk's halo
+#pragma unroll
+                for (int k = 0; k < C; ++k) xq[wv * kWave + (l - (kWave - Geo::HL)) * C + k] = st.cur[k];
+            }
+            WX_T(c1);
             wait_vm();
             __syncthreads();
-            if (q + 1 < nch) stage_rows<VS>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
-                                          lds + ((q + 1) & 1) * kChunk * VS);
-            if (MODE == 0 && lane < rows) q0[q * kChunk + lane] = exp_cr(buf[lane * VS]);  // wave 0
+            WX_T(c2);
+            if (W > 1 && q > 0 && halo) {
+#pragma unroll
+                for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
+            }
+            if (!H) {
+                if (q + 1 < nch)
+                    stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
+                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4);
+                if (MODE == 0 && wv == 0 && l < rows) q0[q * kChunk + l] = exp_cr(buf[l * VS]);  // never idle
+            }
             const char* bb = reinterpret_cast<const char*>(buf);
-            int r = 0;
-            // ---- unrolled groups of kUnroll steps with immediate LDS row offsets
-            for (; r + kUnroll <= rows; r += kUnroll) {
-                const char* gb = bb + r * kRowBytes;
-                const char* ga[C];
-#pragma unroll
-                for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-                if (t + kUnroll < inf_from) {  // every row of the group has a finite column 0
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        step<true>(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f,
-                                   cnt, ring, r + u, gN, N, tr, xch);
-                        ++t;
-                    }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) {
-                        step<false>(gb, ga, u * kRowBytes, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f,
-                                    cnt, ring, r + u, gN, N, tr, xch);
-                        ++t;
-                    }
-                }
-            }
-            // ---- remainder steps (last partial group)
-            for (; r < rows; ++r) {
-                const char* gb = bb + r * kRowBytes;
-                const char* ga[C];
-#pragma unroll
-                for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-                step<false>(gb, ga, 0, boff, cur, w, acc, col0, t, inf_from, lane, is_short, f, cnt, ring, r, gN, N,
-                            tr, xch);
-                ++t;
-            }
-            if (MODE == 0) {
-                reduce_chunk(ring, rows, q * kChunk + 1, best, best_t, nan_t);
-#ifdef WX_DEBUG_RING
-                if (lane < rows) q0[q * kChunk + lane] = ring;
+            const float* c0q = H ? c0b + (q & 1) * kChunk : nullptr;
+            WX_T(c3);
+            if (wv == 0)
+                chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+            else
+                chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+            WX_T(c4);
+#ifdef WX_PHASE_TIMING
+            acc_steps += c4 - c3;
+            acc_bar += c2 - c1;
+            acc_other += (c1 - c0) + (c3 - c2);
 #endif
+            if (MODE == 0) {
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
-                    bits[((int64_t)q * C + k) * kLanes + lane] = (sh == 0) ? w[k] : (w[k] << sh);
-                    w[k] = 0u;
+                    if (!halo) bits[((int64_t)q * C + k) * kLanes + g] = (sh == 0) ? st.w[k] : (st.w[k] << sh);
+                    st.w[k] = 0u;
                 }
             }
         }
-        if (MODE == 0) {
-            const int ts = nan_t > 0 ? nan_t : best_t;  // uniform within each wave
-            if (W == 1) {
-                *t_start_out = ts;
-            } else {  // the owner wave of column N broadcasts through LDS
-                if (uniform(lane >> 6) == (gN >> 6) && (lane & (kWave - 1)) == 0) *tsb = ts;
-                __syncthreads();
-                *t_start_out = *tsb;
+#ifdef WX_PHASE_TIMING
+        if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + wv) * 3;
+            o[0] = acc_steps;
+            o[1] = acc_bar;
+            o[2] = acc_other;
+        }
+#endif
+    }
+
+    // The helper wave (H): mirrors the DP waves' barriers.  Before barrier q, chunks q and
+    // q+1 are staged and column 0 of chunk q is in c0b[q & 1].  (q0 is filled after the
+    // forward pass, while wave 0 walks: fill_q0.)
+    __device__ static void helper(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* c0b,
+                                  int nch, bool x4) {
+        const int T = d.T, N = d.N;
+        const int inf_from = T + 1 - N;
+        double acc = 0.0;  // sum of em[0..t-1, 0], uniform
+        if (nch > 0) stage_rows<VS, 1, true>(E, V, 0, min(kChunk, T), lds, x4);
+        if (nch > 1) stage_rows<VS, 1, true>(E, V, kChunk, min(kChunk, T - kChunk), lds + kChunk * VS, x4);
+        wait_vm();
+        column0(0, T, inf_from, lds, c0b, acc);
+#ifdef WX_PHASE_TIMING
+        unsigned long long acc_c0 = 0, acc_bar = 0, acc_other = 0;
+#endif
+        for (int q = 0; q < nch; ++q) {
+            WX_T(h0);
+            wait_vm();
+            WX_T(h1);
+            __syncthreads();
+            WX_T(h2);
+            if (q + 2 < nch)
+                stage_rows<VS, 1, true>(E, V, (q + 2) * kChunk, min(kChunk, T - (q + 2) * kChunk),
+                                        lds + ((q + 2) % kBufs) * kChunk * VS, x4);
+            WX_T(h3);
+            if (q + 1 < nch) column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
+            WX_T(h4);
+#ifdef WX_PHASE_TIMING
+            acc_c0 += h4 - h3;
+            acc_bar += h2 - h1;
+            acc_other += (h1 - h0) + (h3 - h2);
+#endif
+        }
+#ifdef WX_PHASE_TIMING
+        if (lane_id() == 0 && blockIdx.x < 8192) {
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W) * 3;
+            o[0] = acc_c0;
+            o[1] = acc_bar;
+            o[2] = acc_other;
+        }
+#endif
+    }
+
+    // Column 0 of chunk q (tr[t][0], alignment.py:367-370: 0, fp32(fp64 cumsum), +inf in
+    // the last N rows) into c0b[q & 1][r].  The fp64 chain runs on wave-uniform values (rows
+    // read as LDS broadcasts, converted ahead), one dependent v_add_f64 per row; rows past
+    // the segment's end feed only values nobody reads.
+    __device__ __forceinline__ static void column0(int q, int T, int inf_from, const float* buf, float* c0b,
+                                                   double& acc) {
+        const int t0 = q * kChunk;
+        float* out = c0b + (q & 1) * kChunk;
+        float e[kChunk];
+#pragma unroll
+        for (int r = 0; r < kChunk; ++r) e[r] = buf[r * VS];  // uniform address: broadcast
+#pragma unroll
+        for (int r = 0; r < kChunk; ++r) {
+            out[r] = (float)acc;  // tr[t0 + r][0] before the +inf / row-0 fix-up
+            acc += (double)e[r];
+        }
+        const int l = lane_id();
+        if (l < kChunk) {
+            const int t = t0 + l;
+            const float v = out[l];
+            out[l] = (t >= inf_from) ? INFINITY : (t == 0 ? 0.0f : v);
+        }
+    }
+
+    // One chunk's steps: unrolled groups of kUnroll with immediate LDS row offsets, then the
+    // remainder.  WAVE0: this wave holds column 1 (its left input is column 0).
+    template <bool WAVE0>
+    __device__ __forceinline__ static void chunk(const char* bb, const float* c0q, int rows, const int (&toff)[C],
+                                                 int boff, State& st, int inf_from, bool is_short, bool halo, int f,
+                                                 int cnt, bool owner, int N, float* __restrict__ cn,
+                                                 float* __restrict__ tr) {
+        constexpr int kColLds = 3, kColFinite = 1, kColAny = 2;
+        int r = 0;
+        for (; r + kUnroll <= rows; r += kUnroll) {
+            const char* gb = bb + r * kRowBytes;
+            const char* ga[C];
+#pragma unroll
+            for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
+            float hist[kUnroll];  // column N after each step (owner lane)
+            if (!WAVE0 || H || st.t + kUnroll < inf_from) {  // column 0 from LDS, or finite for the group
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
+                                                                 inf_from, is_short, halo, f, cnt, N, tr);
+                    hist[u] = st.cur[C - 1];
+                    ++st.t;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    step<kColAny>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
+                    hist[u] = st.cur[C - 1];
+                    ++st.t;
+                }
+            }
+            if (MODE == 0 && owner) {  // rows t-7 .. t at cn[t-8 .. t-1] (16-byte aligned)
+                float4* o = reinterpret_cast<float4*>(cn + st.t - kUnroll);
+                o[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
+                o[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
             }
         }
-    }
-
-    // Fold one chunk of column-N values (ring lane i = row t0 + i) into the running argmax
-    // with torch.argmax semantics (first maximum; the first NaN wins and is final).
-    __device__ __forceinline__ static void reduce_chunk(float ring, int rows, int t0, float& best, int& best_t,
-                                                        int& nan_t) {
-        const int l = lane_id();
-        const bool valid = l < rows;
-        const bool isn = valid && (ring != ring);
-        const unsigned long long nm = __ballot(isn);
-        if (nan_t == 0 && nm) nan_t = t0 + (__ffsll((long long)nm) - 1);
-        float v = valid ? ring : -INFINITY;
-        int idx = valid ? l : kChunk;
+        for (; r < rows; ++r) {
+            const char* gb = bb + r * kRowBytes;
+            const char* ga[C];
 #pragma unroll
-        for (int off = 1; off < kChunk; off <<= 1) {  // (max, first index), NaN rows excluded
-            const float v2 = __shfl_xor(v, off);
-            const int i2 = __shfl_xor(idx, off);
-            const bool take = (v2 > v) || (v2 == v && i2 < idx) || (v != v && v2 == v2);
-            v = take ? v2 : v;
-            idx = take ? i2 : idx;
-        }
-        v = __shfl(v, 0);
-        idx = __shfl(idx, 0);
-        if (v == v && v > best && idx < rows) {
-            best = v;
-            best_t = t0 + idx;
+            for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
+            step<!WAVE0 ? 0 : (H ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
+                                                       cnt, N, tr);
+            if (MODE == 0 && owner) cn[st.t] = st.cur[C - 1];
+            ++st.t;
         }
     }
 
-    template <bool FINITE_COL0>
+    // One time step t -> t+1 (alignment.py:372-378).  COL: 0 = not the column-1 wave (lane
+    // 0's left input is a halo edge, don't-care); column-1 wave: 1 = column 0 finite for the
+    // next row, 2 = general column 0, 3 = column 0 read from the helper's LDS row.
+    template <int COL>
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
-                                                cellvec<C>& cur, unsigned (&w)[C], double& acc, float& col0,
-                                                int t, int inf_from, int lane, bool is_short, int f, int cnt,
-                                                float& ring, int r, int gN, int N, float* __restrict__ tr,
-                                                float* xch) {
+                                                const float* c0, State& st, int inf_from, bool is_short, bool halo,
+                                                int f, int cnt, int N, float* __restrict__ tr) {
         const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
-        const float e0 = *reinterpret_cast<const float*>(gb + ro);
         float et[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
         // last cell of the lane to the left (short lanes end at slot C-2)
-        const float src = (C > 1 && is_short) ? cur[C > 1 ? C - 2 : 0] : cur[C - 1];
-        float in0 = col0;  // what lane 0 of this wave sees on its left
-        if constexpr (W > 1) {
-            const int wv = lane >> 6;
-            float* slot = xch + (t & 1) * W;
-            if ((lane & (kWave - 1)) == kWave - 1) slot[wv] = src;
-            __syncthreads();
-            if (wv > 0) in0 = slot[wv - 1];
-        }
+        const float src = (C > 1 && is_short) ? st.cur[C > 1 ? C - 2 : 0] : st.cur[C - 1];
+        const float in0 = COL == 3 ? *c0 : (COL ? st.col0 : src);
         const float left = dpp_shr1(in0, src);
 #pragma unroll
         for (int k = C - 1; k >= 0; --k) {
-            const float s = cur[k] + eb;
-            const float c = (k == 0 ? left : cur[k > 0 ? k - 1 : 0]) + et[k];
-            if (MODE == 0) w[k] = shift_in(w[k], c, s);
-            cur[k] = nan_max(s, c);
+            const float s = st.cur[k] + eb;
+            const float c = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
+            if (MODE == 0) st.w[k] = shift_in(st.w[k], c, s);
+            st.cur[k] = nan_max(s, c);
         }
-        acc += (double)e0;
-        col0 = (FINITE_COL0 || t + 1 < inf_from) ? (float)acc : INFINITY;
-        if (MODE == 0) {
-            // column N = slot C-1 of lane gN.  The empty asm pins the operand: without it
-            // hipcc (ROCm 7.2) folded this readlane into the DPP-source select above and read
-            // slot C-2 (caught by the golden tests).
-            float vN = cur[C - 1];
-            asm("" : "+v"(vN));  // opaque, but not a scheduling barrier
-            const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vN),
-                                                                               gN & (kWave - 1)));
-            ring = (lane_id() == r) ? v : ring;  // v_cmp_eq + v_cndmask; hazards handled by hipcc
-        } else {
-            float* row = tr + (int64_t)(t + 1) * ((int64_t)N + 1);
-            if (lane == 0) row[0] = col0;
+        if (COL == 1 || COL == 2) {
+            const float e0 = *reinterpret_cast<const float*>(gb + ro);
+            st.acc += (double)e0;
+            st.col0 = (COL == 1 || st.t + 1 < inf_from) ? (float)st.acc : INFINITY;
+        }
+        if (MODE == 1) {
+            float* row = tr + (int64_t)(st.t + 1) * ((int64_t)N + 1);
+            if (COL && lane_id() == 0)
+                row[0] = COL == 3 ? (st.t + 1 < inf_from ? c0[1] : INFINITY) : st.col0;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 const int j = f + k;
-                if (k < cnt && j <= N) row[j] = cur[k];
+                if (!halo && k < cnt && j <= N) row[j] = st.cur[k];
             }
         }
     }
 };
+
+// q0[t] = exp(em[t, 0]) for rows [0, T), by the threads [first_thread, blockDim) (the waves
+// that do not walk).
+__device__ void fill_q0(const float* __restrict__ E, int V, int T, float* __restrict__ q0, int first_thread) {
+    const int n = (int)blockDim.x - first_thread;
+    for (int t = (int)threadIdx.x - first_thread; t < T; t += n) q0[t] = exp_cr(E[(int64_t)t * V]);
+}
+
+// Argmax of column N over rows 0..T with torch.argmax semantics (first maximum; the first
+// NaN wins), rows 1..T read from cn[0..T-1], row 0 = -inf (alignment.py:395-396).  Wave 0.
+__device__ int column_argmax(const float* __restrict__ cn, int T) {
+    const int l = lane_id();
+    int nan_row = 0x7fffffff, best_row = 0;
+    float best = -INFINITY;
+    for (int i = l; i < T; i += kWave) {
+        const float v = cn[i];
+        if (v != v) {
+            nan_row = min(nan_row, i + 1);
+        } else if (v > best) {
+            best = v;
+            best_row = i + 1;
+        }
+    }
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        nan_row = min(nan_row, __shfl_xor(nan_row, off));
+        const float b2 = __shfl_xor(best, off);
+        const int r2 = __shfl_xor(best_row, off);
+        if (b2 > best || (b2 == best && r2 < best_row)) {
+            best = b2;
+            best_row = r2;
+        }
+    }
+    return uniform(nan_row != 0x7fffffff ? nan_row : best_row);
+}
 
 // ------------------------------------------------------------------------------------
 // Backtrack walk over the decision bitmap (alignment.py:395-421).  Uniform control flow,
 // executed by the whole wave; `lay` maps cells to the bitmap's (lane, slot) words.
 // Records start[k] = first frame of token k (the frame where the path moved onto it).
 // Returns true on success (j reached 0), false where the reference returns None.
+template <int CC>
 __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bits, const Layout& lay, int b, int A) {
     const int jj = A - lane_id();
     if (jj < 1) return 0u;
     int g, k;
-    lay.locate(jj - 1, g, k);
+    lay.locate<CC>(jj - 1, g, k);
     return bits[((int64_t)b * lay.C + k) * lay.lanes + g];
 }
 
-// Walk one 32-step block (decision indices 32b+s_hi .. 32b) from window offset d.
-// Purely scalar: the only vector instruction is the v_readlane of the column word.
-// Returns the block's change mask (bit 31-s = the path moved onto a new token at 32b+s).
-template <bool FULL>
-__device__ __forceinline__ unsigned walk_block(unsigned win, int& d, int s_hi) {
+// Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d; steps
+// before the walk's start must have their bits cleared.  The block's bit columns are first
+// transposed into SGPR ballots (mask_s bit i = decision bit of window lane i at step s), so
+// the serial part is a pure SALU chain per step — SCC = mask_s[d]; d += SCC — with no
+// VALU <-> SALU round trip.  Returns the change mask (bit 31-s = the path moved onto a new
+// token at 32b+s).
+__device__ __forceinline__ unsigned walk_block(unsigned win, int& d) {
     unsigned cm = 0u;
-    if (FULL) {
 #pragma unroll
-        for (int s = 31; s >= 0; --s) {
-            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, d);
-            const unsigned bit = (word >> (31 - s)) & 1u;
-            cm |= bit << (31 - s);
-            d += (int)bit;
-        }
-    } else {
-        for (int s = s_hi; s >= 0; --s) {
-            const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)win, d);
-            const unsigned bit = (word >> (31 - s)) & 1u;
-            cm |= bit << (31 - s);
-            d = uniform(d + (int)bit);
-        }
+    for (int s0 = 31; s0 >= 0; s0 -= 8) {
+        unsigned long long m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = __ballot((win >> (31 - (s0 - i))) & 1u);
+        // all 8 ballots are issued before the chain reads the first (hipcc would otherwise
+        // sink each v_cmp next to its reader and expose the VALU -> SGPR latency per step)
+        asm volatile("" ::"s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7]));
+        unsigned t0, t1;
+#define WX_WALK_STEP(I, T)                        \
+    "s_bitcmp1_b64 %[m" #I "], %[d]\n\t"          \
+    "s_cselect_b32 %[" #T "], %[k" #I "], 0\n\t" \
+    "s_addc_u32 %[d], %[d], 0\n\t"                \
+    "s_or_b32 %[cm], %[cm], %[" #T "]\n\t"
+        asm volatile(WX_WALK_STEP(0, t0) WX_WALK_STEP(1, t1) WX_WALK_STEP(2, t0) WX_WALK_STEP(3, t1)
+                         WX_WALK_STEP(4, t0) WX_WALK_STEP(5, t1) WX_WALK_STEP(6, t0) WX_WALK_STEP(7, t1)
+                     : [d] "+s"(d), [cm] "+s"(cm), [t0] "=&s"(t0), [t1] "=&s"(t1)
+                     : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3]), [m4] "s"(m[4]),
+                       [m5] "s"(m[5]), [m6] "s"(m[6]), [m7] "s"(m[7]), [k0] "i"(1u << (31 - s0)),
+                       [k1] "i"(1u << (32 - s0)), [k2] "i"(1u << (33 - s0)), [k3] "i"(1u << (34 - s0)),
+                       [k4] "i"(1u << (35 - s0)), [k5] "i"(1u << (36 - s0)), [k6] "i"(1u << (37 - s0)),
+                       [k7] "i"(1u << (38 - s0))
+                     : "scc");
+#undef WX_WALK_STEP
     }
     return cm;
 }
@@ -442,16 +665,18 @@ __device__ __forceinline__ unsigned walk_block(unsigned win, int& d, int s_hi) {
 // without an early-exit test.  Per block only the change mask is kept (cmask[b]);
 // start frames are compacted from it afterwards.  Returns the lowest block touched, or -1
 // where the reference returns None.
+template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
 __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask) {
     if (t_start <= 0 || N <= 0) return -1;
     int j = N;
     int b = (t_start - 1) >> 5;
     int A = j;
-    unsigned win = load_window(bits, lay, b, A);
+    const int s_hi = (t_start - 1) & 31;  // steps above t_start-1 do not exist: clear their bits
+    unsigned win = load_window<CC>(bits, lay, b, A) & (0xFFFFFFFFu << (31 - s_hi));
     int An = A;
-    unsigned nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
+    unsigned nxt = (b > 0) ? load_window<CC>(bits, lay, b - 1, An) : 0u;
     int d = 0;
-    unsigned cm = walk_block<false>(win, d, (t_start - 1) & 31);
+    unsigned cm = walk_block(win, d);
     while (true) {
         cmask[b] = cm;
         j = uniform(A - d);
@@ -461,9 +686,9 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
         win = nxt;
         A = An;
         An = j;
-        nxt = (b > 0) ? load_window(bits, lay, b - 1, An) : 0u;
+        nxt = (b > 0) ? load_window<CC>(bits, lay, b - 1, An) : 0u;
         d = A - j;
-        cm = walk_block<true>(win, d, 31);
+        cm = walk_block(win, d);
     }
 }
 
@@ -523,29 +748,43 @@ __device__ __forceinline__ void block_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// (cells per lane C, waves per segment W) buckets, one kernel instantiation each.
-// Single-wave buckets cover N <= 2048; longer transcripts use W waves that exchange the
-// boundary cell through LDS once per step.
-#define WX_BUCKETS(X) \
-    X(1, 1) X(2, 1) X(4, 1) X(6, 1) X(8, 1) X(12, 1) X(16, 1) X(24, 1) X(32, 1) X(16, 4) X(16, 8) X(32, 8)
+// (cells per lane C, DP waves per segment W, helper wave H) buckets, one kernel
+// instantiation each; id = C << 8 | W << 1 | H.
+// Throughput mode (many segments in flight): one wave per segment up to N = 2048; longer
+// transcripts use W waves with a chunk halo (Geometry).  Latency mode (few segments: the
+// chip would otherwise be mostly idle): a segment's columns are spread over 3 or 7 waves
+// plus the helper (at most 2 waves per SIMD, which still issue at the full rate), so each
+// wave issues fewer instructions per time step.
+#define WX_BUCKETS(X)                                                                                         \
+    X(1, 1, 0) X(2, 1, 0) X(4, 1, 0) X(6, 1, 0) X(8, 1, 0) X(12, 1, 0) X(16, 1, 0) X(24, 1, 0) X(32, 1, 0)    \
+        X(16, 4, 0) X(16, 8, 0) X(32, 8, 0) X(1, 3, 1) X(1, 7, 1) X(2, 3, 1) X(2, 7, 1) X(4, 7, 1) X(8, 7, 1)
 
-__host__ __device__ __forceinline__ int bucket_id(int N) {  // = C * 64 + W
-    const int need = (N + kWave - 1) / kWave;
-    if (need <= 1) return 1 * 64 + 1;
-    if (need <= 2) return 2 * 64 + 1;
-    if (need <= 4) return 4 * 64 + 1;
-    if (need <= 6) return 6 * 64 + 1;
-    if (need <= 8) return 8 * 64 + 1;
-    if (need <= 12) return 12 * 64 + 1;
-    if (need <= 16) return 16 * 64 + 1;
-    if (need <= 24) return 24 * 64 + 1;
-    if (need <= 32) return 32 * 64 + 1;
-    if (need <= 64) return 16 * 64 + 4;
-    if (need <= 128) return 16 * 64 + 8;
-    return 32 * 64 + 8;
+__host__ __device__ constexpr int bucket_make(int C, int W, int H) { return (C << 8) | (W << 1) | H; }
+__host__ __device__ constexpr int bucket_C(int id) { return id >> 8; }
+__host__ __device__ constexpr int bucket_W(int id) { return (id >> 1) & 127; }
+
+__host__ __device__ constexpr int bucket_capacity(int C, int W) {
+    return C * (kWave + (W - 1) * (kWave - (W > 1 ? (32 + C - 1) / C : 0)));
 }
 
-__host__ __device__ __forceinline__ int bucket_cells_total(int id) { return (id / 64) * kWave * (id % 64); }
+// Buckets of each mode in increasing capacity (compare chains: a dynamically indexed
+// table would live in scratch on the device).
+#define WX_PICK(CC, WW, HH) \
+    if (N <= bucket_capacity(CC, WW)) return bucket_make(CC, WW, HH);
+__host__ __device__ __forceinline__ int bucket_id(int N, int mode = 0) {
+    if (mode == 1) {
+        WX_PICK(1, 1, 0) WX_PICK(1, 3, 1) WX_PICK(1, 7, 1) WX_PICK(2, 3, 1) WX_PICK(2, 7, 1) WX_PICK(4, 7, 1)
+        WX_PICK(8, 7, 1) WX_PICK(16, 8, 0)
+    } else {
+        WX_PICK(1, 1, 0) WX_PICK(2, 1, 0) WX_PICK(4, 1, 0) WX_PICK(6, 1, 0) WX_PICK(8, 1, 0) WX_PICK(12, 1, 0)
+        WX_PICK(16, 1, 0) WX_PICK(24, 1, 0) WX_PICK(32, 1, 0) WX_PICK(16, 4, 0) WX_PICK(16, 8, 0)
+    }
+    return bucket_make(32, 8, 0);
+}
+#undef WX_PICK
+
+// bitmap words per 32-step block of a segment in bucket `id`
+__host__ __device__ __forceinline__ int bucket_cells_total(int id) { return bucket_C(id) * kWave * bucket_W(id); }
 
 struct AlignArgs {
     const float* em;
@@ -555,6 +794,8 @@ struct AlignArgs {
     const int64_t* tok_off;
     const int32_t* blank_id;
     int S;
+    int mode;  // 0 throughput buckets, 1 latency buckets
+    int x4;    // V == 32 and 16-byte aligned rows: 16-byte LDS staging
     int32_t* seg_start;
     int32_t* seg_end;
     double* seg_score;
@@ -564,17 +805,20 @@ struct AlignArgs {
     int bits_stride_cells;  // 64 * Cstride dwords per block
     float* q0;       // workspace: sum_T floats
     unsigned* cmask; // workspace: walk change masks, (floor(row0/32) + seg) words per segment
+    float* cn;       // workspace: column N history, segment at (row0 + 4 seg) & ~3
 };
 
-template <int C, int VS, int W>
-__global__ __launch_bounds__(kWave * W) void align_dp_kernel(AlignArgs a) {
-    __shared__ float lds[2 * kChunk * VS];
+
+template <int C, int VS, int W, int H>
+__global__ __launch_bounds__(kWave*(W + H)) void align_dp_kernel(AlignArgs a) {
+    __shared__ float lds[(H ? 3 : 2) * kChunk * VS];
+    __shared__ float c0b[H ? 2 * kChunk : 1];
+    __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
-    __shared__ float xch[2 * W];
     __shared__ int tsb[2];
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
-    if (bucket_id(d.N) != C * 64 + W) return;  // another instantiation owns this segment
+    if (bucket_id(d.N, a.mode) != bucket_make(C, W, H)) return;  // another instantiation owns it
     const int lane = (int)threadIdx.x;
     if (d.N <= 0 || d.T <= 0) {
         if (lane == 0) {
@@ -586,27 +830,40 @@ __global__ __launch_bounds__(kWave * W) void align_dp_kernel(AlignArgs a) {
     const float* E = a.em + d.row0 * a.V;
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
-    int ts = 0;
-    Forward<C, VS, 0, W>::run(d, E, a.V, a.tok, bits, q0, nullptr, &ts, lds, xch, tsb);
-    if (lane == 0) a.t_start[seg] = ts;
+    float* cn = a.cn + ((d.row0 + 4 * (int64_t)seg) & ~(int64_t)3);
+    WX_STAMP_RT(4);
+    WX_STAMP(0);
+    Forward<C, VS, 0, W, H != 0>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0);
+    WX_STAMP(1);
     wait_vm();
     block_fence();
     int32_t* start = a.seg_start + d.tok0;
-    if (lane < kWave) {  // wave 0 walks, then compacts the change masks into start frames
+    if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
+        const int ts = column_argmax(cn, d.T);
+        if (lane == 0) {
+            a.t_start[seg] = ts;
+            tsb[0] = ts;
+        }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk(bits, Layout::make(C, d.N, kWave * W), d.N, ts, cmask);
+        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W), d.N, ts, cmask);
         if (b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
         }
         if (lane == 0) tsb[1] = b_lo >= 0 ? 1 : 0;
+    } else if (H) {
+        fill_q0(E, a.V, d.T, q0, kWave);
     }
     wait_vm();
     block_fence();
+    const int ts = tsb[0];
     const bool ok = tsb[1] != 0;
+    WX_STAMP(2);
     if (lane == 0) a.status[seg] = ok ? 0 : 1;
     if (!ok) return;
     merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
+    WX_STAMP(3);
+    WX_STAMP_RT(5);
 }
 
 struct TrellisArgs {
@@ -618,15 +875,16 @@ struct TrellisArgs {
     const int32_t* blank_id;
     float* tr;
     const int64_t* tr_off;
+    int x4;
 };
 
 template <int C, int VS, int W>
 __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
     __shared__ float lds[2 * kChunk * VS];
-    __shared__ float xch[2 * W];
+    __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
-    if (bucket_id(d.N) != C * 64 + W) return;
+    if (bucket_id(d.N) != bucket_make(C, W, 0)) return;
     float* tr = a.tr + a.tr_off[seg];
     const int lane = (int)threadIdx.x;
     if (d.N == 0) {  // the whole single column is +inf (alignment.py:369-370 with num_tokens = 0)
@@ -634,7 +892,7 @@ __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
         return;
     }
     const float* E = a.em + d.row0 * a.V;
-    Forward<C, VS, 1, W>::run(d, E, a.V, a.tok, nullptr, nullptr, tr, nullptr, lds, xch, nullptr);
+    Forward<C, VS, 1, W, false>::run(d, E, a.V, a.tok, nullptr, nullptr, nullptr, tr, lds, nullptr, xh, a.x4 != 0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -752,7 +1010,7 @@ __global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
         lay.n_short = 0;
         lay.lanes = kWave;
         unsigned* cmask = a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk(bits, lay, N, ts, cmask);
+        const int b_lo = walk<0>(bits, lay, N, ts, cmask);
         if (b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
@@ -1096,15 +1354,29 @@ int fork_join(hipStream_t st, int n, F&& launch) {
 
 // bucket ids in launch order, ids = C*64 + W
 constexpr int kBucketIds[] = {
-#define WX_ID(CC, WW) CC * 64 + WW,
+#define WX_ID(CC, WW, HH) bucket_make(CC, WW, HH),
     WX_BUCKETS(WX_ID)
 #undef WX_ID
 };
 constexpr int kNumBuckets = sizeof(kBucketIds) / sizeof(int);
 
+// The buckets that segments with N in [min_N, max_N] map to (N == 0 -> the first one).
+int buckets_for(int64_t min_N, int64_t max_N, int mode, int* ids) {
+    int n = 0;
+    int64_t N = std::max<int64_t>(min_N, 1);
+    const int64_t hi = std::max<int64_t>(max_N, 1);
+    while (N <= hi) {
+        const int id = bucket_id((int)N, mode);
+        ids[n++] = id;
+        N = (int64_t)bucket_capacity(bucket_C(id), bucket_W(id)) + 1;
+    }
+    return n;
+}
+
 // bitmap: per segment (floor(row0/32) + seg) block offsets, 64 * C_stride dwords per block
 size_t bitmap_bytes(int32_t S, int64_t sum_T, int64_t max_N, int* stride_cells) {
-    const int cells = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
+    const int nmax = (int)std::max<int64_t>(max_N, 1);  // widest bucket of either mode
+    const int cells = std::max(bucket_cells_total(bucket_id(nmax, 0)), bucket_cells_total(bucket_id(nmax, 1)));
     if (stride_cells) *stride_cells = cells;
     const int64_t blocks = sum_T / kChunk + S + 1;
     return align_up((size_t)blocks * (size_t)cells * 4u, 256);
@@ -1121,23 +1393,48 @@ const char* wx_strerror(int code) {
         case WX_OK: return "ok";
         case WX_E_INVALID: return "invalid argument";
         case WX_E_VOCAB: return "vocabulary size outside [1, 64]";
-        case WX_E_TOO_LONG: return "segment has more than 16384 tokens";
+        case WX_E_TOO_LONG: return "segment has more than 16000 tokens";
         case WX_E_WORKSPACE: return "workspace too small";
         case WX_E_LAUNCH: return "kernel launch failed";
         default: return hipGetErrorString((hipError_t)code);
     }
 }
 
+// Launch shape: latency buckets while the batch cannot fill the chip with one wave per
+// segment.  WX_ALIGN_MODE=0/1 forces a shape for WX_MODE_AUTO calls (benchmarking only).
+int align_mode(int32_t S, int32_t mode) {
+    if (mode == WX_MODE_THROUGHPUT || mode == WX_MODE_LATENCY) return mode;
+    static const int forced = [] {
+        const char* e = getenv("WX_ALIGN_MODE");
+        return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : -1;
+    }();
+    if (forced >= 0) return forced;
+    return S <= 256 ? WX_MODE_LATENCY : WX_MODE_THROUGHPUT;
+}
+
 size_t cmask_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T / kChunk + S + 1) * 4u, 256); }
 
+// column N history: segment s at (row0 + 4 s) & ~3 (16-byte aligned groups of 8 rows)
+size_t cn_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T + 4 * (int64_t)S + 16) * 4u, 256); }
+
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
-    return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T);
+    return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T) +
+           cn_bytes(S, sum_T);
 }
 
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
                 const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T, int32_t* seg_start,
                 int32_t* seg_end, double* seg_score, int32_t* t_start, int32_t* status, void* workspace,
                 size_t workspace_bytes, void* stream) {
+    return wx_align_dp_mode(em, em_off, V, tok, tok_off, blank_id, S, min_N, max_N, sum_T, seg_start, seg_end,
+                            seg_score, t_start, status, workspace, workspace_bytes, WX_MODE_AUTO, stream);
+}
+
+int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok,
+                     const int64_t* tok_off, const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N,
+                     int64_t sum_T, int32_t* seg_start, int32_t* seg_end, double* seg_score, int32_t* t_start,
+                     int32_t* status, void* workspace, size_t workspace_bytes, int32_t mode, void* stream) {
+    if (mode < WX_MODE_AUTO || mode > WX_MODE_LATENCY) return WX_E_INVALID;
     if (S < 0 || sum_T < 0 || min_N < 0 || max_N < min_N) return WX_E_INVALID;
     if (S == 0) return WX_OK;
     if (!em || !em_off || !tok_off || !blank_id || !seg_start || !seg_end || !seg_score || !t_start || !status ||
@@ -1154,21 +1451,19 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t
     a.q0 = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + bm);
     a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
                                           align_up((size_t)(sum_T + 1) * 4u, 256));
+    a.cn = reinterpret_cast<float*>(reinterpret_cast<char*>(a.cmask) + cmask_bytes(S, sum_T));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // buckets are ordered by capacity; N == 0 segments belong to the first one
-    const int lo = bucket_cells_total(bucket_id((int)std::max<int64_t>(min_N, 1)));
-    const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
-    int ids[kNumBuckets], n = 0;
-    for (int i = 0; i < kNumBuckets; ++i) {
-        const int cells = bucket_cells_total(kBucketIds[i]);
-        if (cells >= lo && cells <= hi) ids[n++] = kBucketIds[i];
-    }
+    a.mode = align_mode(S, mode);
+    a.x4 = (V == 32 && (reinterpret_cast<uintptr_t>(em) & 15) == 0) ? 1 : 0;
+    int ids[kNumBuckets];
+    const int n = buckets_for(min_N, max_N, a.mode, ids);
     const dim3 grid(S);
     return fork_join(st, n, [&](int i, hipStream_t s) {
-#define WX_LAUNCH_ALIGN(CC, WW)                                                                          \
-        if (ids[i] == CC * 64 + WW) {                                                                  \
-            if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
-            else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a);         \
+#define WX_LAUNCH_ALIGN(CC, WW, HH)                                                                  \
+        if (ids[i] == bucket_make(CC, WW, HH)) {                                                       \
+            const dim3 block(kWave * (WW + HH));                                                       \
+            if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW, HH>), grid, block, 0, s, a);   \
+            else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW, HH>), grid, block, 0, s, a);           \
         }
         WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
@@ -1187,14 +1482,13 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
     a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id;
     a.tr = trellis; a.tr_off = tr_off;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int hi = bucket_cells_total(bucket_id((int)std::max<int64_t>(max_N, 1)));
-    int ids[kNumBuckets], n = 0;
-    for (int i = 0; i < kNumBuckets; ++i)
-        if (bucket_cells_total(kBucketIds[i]) <= hi) ids[n++] = kBucketIds[i];
+    a.x4 = (V == 32 && (reinterpret_cast<uintptr_t>(em) & 15) == 0) ? 1 : 0;
+    int ids[kNumBuckets];
+    const int n = buckets_for(0, max_N, 0, ids);
     const dim3 grid(S);
     return fork_join(st, n, [&](int i, hipStream_t s) {
-#define WX_LAUNCH_TR(CC, WW)                                                                            \
-        if (ids[i] == CC * 64 + WW) {                                                                 \
+#define WX_LAUNCH_TR(CC, WW, HH)                                                                        \
+        if (!HH && ids[i] == bucket_make(CC, WW, 0)) {                                                \
             if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
             else hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a);         \
         }
@@ -1272,3 +1566,14 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, cons
 }
 
 }  // extern "C"
+
+#ifdef WX_PHASE_TIMING
+extern "C" int wx_debug_phases(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_phase), sizeof(unsigned long long) * 6 * (size_t)n, 0,
+                                    hipMemcpyDeviceToHost);
+}
+extern "C" int wx_debug_loop(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_loop), sizeof(unsigned long long) * 48 * (size_t)n, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
