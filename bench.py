@@ -64,6 +64,20 @@ def algorithmic_bytes(Ts, Ns, V):
     return int(sum(4 * T * V + 4 * N + (T * N) // 8 + 16 * N for T, N in zip(Ts, Ns)))
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes over this same
+    command, gfx950 FETCH_SIZE correction applied) — or None when none matches."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("kernel") == kernel:
+            return int(d["traffic_bytes_per_launch"]), os.path.basename(f)
+    return None, None
+
+
 def time_steps(plan, steps, warmup, dist_on):
     for _ in range(warmup):
         plan.run()
@@ -72,17 +86,21 @@ def time_steps(plan, steps, warmup, dist_on):
         torch.distributed.barrier()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # one event pair around every step on the stream the kernel runs on (a config-2 batch
+    # maps to one bucket, which wx_align_dp launches directly on the caller's stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
+    for a, b in ev:
+        a.record(stream)
         plan.run()
-    e1.record(stream)
+        b.record(stream)
     torch.cuda.synchronize()
     if dist_on:
         torch.distributed.barrier()
     host_s = time.perf_counter() - t0
-    dev_s = e0.elapsed_time(e1) / 1000.0
+    launch_s = [a.elapsed_time(b) / 1000.0 for a, b in ev]
+    dev_s = ev[0][0].elapsed_time(ev[-1][1]) / 1000.0
+    time_steps.last_launch_s = float(np.mean(launch_s))
     return host_s, dev_s
 
 
@@ -216,7 +234,10 @@ def main():
     out = None
     if rank == 0:
         B = algorithmic_bytes(batch.Ts, batch.Ns, V)
-        achieved = B / (dev_s / args.steps) / 1e9
+        launch_s = time_steps.last_launch_s  # HIP events around each step's kernel
+        achieved = B / launch_s / 1e9
+        kname = f"void wx::align_dp_kernel<2, {32 if V <= 32 else 64}, 7, 1>(wx::AlignArgs)"
+        traffic, traffic_src = pmc_traffic(kname)
         out = {
             "metric": "aligned audio-sec/s + word-boundary MAE(ms) vs ref, 1/2/4/8 GPU",
             "value": value,
@@ -235,9 +256,10 @@ def main():
                        "global_batch": args.segments * world, "seq_len": T,
                        "parallelism": f"dp{world} (per-file sharding, RCCL vocab broadcast)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": "align_dp_kernel (all buckets of the step, fork-joined)",
-                         "bytes_per_step": B},
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "align_dp_kernel<2,32,7,1> (the step's only launch: all 64 segments, "
+                                   "N 257..704 bucket)",
+                         "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6},
         }
         mae, ntok, nbad = mae_vs_oracle([e.cpu().numpy() for e in ems], toks, plan)
         out["mae_ms"] = mae

@@ -128,7 +128,7 @@ def _capacity(C, W):
 
 
 THROUGHPUT_BUCKETS = [(1, 1), (2, 1), (4, 1), (6, 1), (8, 1), (12, 1), (16, 1), (24, 1), (32, 1), (16, 4), (16, 8)]
-LATENCY_BUCKETS = [(1, 1), (1, 3), (1, 7), (2, 3), (2, 7), (4, 7), (8, 7), (16, 8)]
+LATENCY_BUCKETS = [(1, 1), (1, 3), (1, 7), (2, 7), (4, 7), (8, 7), (16, 8)]
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -493,6 +493,11 @@ struct Forward {
                                                  int cnt, bool owner, int N, float* __restrict__ cn,
                                                  float* __restrict__ tr) {
         constexpr int kColLds = 3, kColFinite = 1, kColAny = 2;
+        if (H && rows == kChunk) {  // latency buckets: software-pipelined full chunk
+            pipelined_chunk<WAVE0 ? kColLds : 0>(bb, c0q, toff, boff, st, WAVE0 && is_short, halo, f, cnt, owner, N,
+                                                 cn, tr);
+            return;
+        }
         int r = 0;
         for (; r + kUnroll <= rows; r += kUnroll) {
             const char* gb = bb + r * kRowBytes;
@@ -534,6 +539,40 @@ struct Forward {
         }
     }
 
+    // A full 32-step chunk with the LDS operands of step u+2 and u+3 loaded while step u
+    // computes.  sched_barrier keeps the scheduler from sinking the loads back to their uses
+    // (it does, to minimise registers); the waitcnt pass counts them exactly, since LDS
+    // returns in order.
+    template <int COL>
+    __device__ __forceinline__ static void pipelined_chunk(const char* bb, const float* c0q, const int (&toff)[C],
+                                                           int boff, State& st, bool is_short, bool halo, int f,
+                                                           int cnt, bool owner, int N, float* __restrict__ cn,
+                                                           float* __restrict__ tr) {
+        const char* ga[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) ga[k] = bb + toff[k];
+        Row rw[kChunk];
+        load_row<COL>(bb, ga, 0, boff, c0q, rw[0]);
+        load_row<COL>(bb, ga, kRowBytes, boff, c0q + 1, rw[1]);
+        float hist[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) {
+            if ((u & 1) == 0 && u + 2 < kChunk) {
+                load_row<COL>(bb, ga, (u + 2) * kRowBytes, boff, c0q + u + 2, rw[u + 2]);
+                load_row<COL>(bb, ga, (u + 3) * kRowBytes, boff, c0q + u + 3, rw[u + 3]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, 0x7fffffff, is_short, halo, f, cnt, N, tr);
+            hist[u & (kUnroll - 1)] = st.cur[C - 1];
+            ++st.t;
+            if (MODE == 0 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
+                float4* o = reinterpret_cast<float4*>(cn + st.t - kUnroll);
+                o[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
+                o[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+            }
+        }
+    }
+
     // One time step t -> t+1 (alignment.py:372-378).  COL: 0 = not the column-1 wave (lane
     // 0's left input is a halo edge, don't-care); column-1 wave: 1 = column 0 finite for the
     // next row, 2 = general column 0, 3 = column 0 read from the helper's LDS row.
@@ -541,13 +580,35 @@ struct Forward {
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 const float* c0, State& st, int inf_from, bool is_short, bool halo,
                                                 int f, int cnt, int N, float* __restrict__ tr) {
-        const float eb = *reinterpret_cast<const float*>(gb + ro + boff);
+        Row rw;
+        load_row<COL>(gb, ga, ro, boff, c0, rw);
+        advance<COL>(gb, ro, c0, rw, st, inf_from, is_short, halo, f, cnt, N, tr);
+    }
+
+    // The LDS operands of one step: em[t, blank], em[t, tok[j-1]] per slot, column 0 (COL 3).
+    struct Row {
+        float eb;
         float et[C];
+        float c0;
+    };
+    template <int COL>
+    __device__ __forceinline__ static void load_row(const char* gb, const char* (&ga)[C], int ro, int boff,
+                                                    const float* c0, Row& rw) {
+        rw.eb = *reinterpret_cast<const float*>(gb + ro + boff);
 #pragma unroll
-        for (int k = 0; k < C; ++k) et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
+        for (int k = 0; k < C; ++k) rw.et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
+        if (COL == 3) rw.c0 = *c0;
+    }
+
+    template <int COL>
+    __device__ __forceinline__ static void advance(const char* gb, int ro, const float* c0, const Row& rw, State& st,
+                                                   int inf_from, bool is_short, bool halo, int f, int cnt, int N,
+                                                   float* __restrict__ tr) {
+        const float eb = rw.eb;
+        const float(&et)[C] = rw.et;
         // last cell of the lane to the left (short lanes end at slot C-2)
         const float src = (C > 1 && is_short) ? st.cur[C > 1 ? C - 2 : 0] : st.cur[C - 1];
-        const float in0 = COL == 3 ? *c0 : (COL ? st.col0 : src);
+        const float in0 = COL == 3 ? rw.c0 : (COL ? st.col0 : src);
         const float left = dpp_shr1(in0, src);
 #pragma unroll
         for (int k = C - 1; k >= 0; --k) {
@@ -587,13 +648,23 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
     const int l = lane_id();
     int nan_row = 0x7fffffff, best_row = 0;
     float best = -INFINITY;
-    for (int i = l; i < T; i += kWave) {
-        const float v = cn[i];
-        if (v != v) {
-            nan_row = min(nan_row, i + 1);
-        } else if (v > best) {
-            best = v;
-            best_row = i + 1;
+    constexpr int kBatch = 8;  // loads in flight per lane
+    for (int base = 0; base < T; base += kBatch * kWave) {
+        float v[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+            const int i = base + u * kWave + l;
+            v[u] = i < T ? cn[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {  // rows of a lane in increasing order
+            const int row = base + u * kWave + l + 1;
+            if (v[u] != v[u]) {
+                nan_row = min(nan_row, row);
+            } else if (v[u] > best) {
+                best = v[u];
+                best_row = row;
+            }
         }
     }
 #pragma unroll
@@ -754,10 +825,11 @@ __device__ __forceinline__ void block_fence() {
 // transcripts use W waves with a chunk halo (Geometry).  Latency mode (few segments: the
 // chip would otherwise be mostly idle): a segment's columns are spread over 3 or 7 waves
 // plus the helper (at most 2 waves per SIMD, which still issue at the full rate), so each
-// wave issues fewer instructions per time step.
+// wave issues fewer instructions per time step.  (Waves beyond column N only keep the
+// barrier count, so a wide bucket costs no time: 30 s segments, N 257..704, share one.)
 #define WX_BUCKETS(X)                                                                                         \
     X(1, 1, 0) X(2, 1, 0) X(4, 1, 0) X(6, 1, 0) X(8, 1, 0) X(12, 1, 0) X(16, 1, 0) X(24, 1, 0) X(32, 1, 0)    \
-        X(16, 4, 0) X(16, 8, 0) X(32, 8, 0) X(1, 3, 1) X(1, 7, 1) X(2, 3, 1) X(2, 7, 1) X(4, 7, 1) X(8, 7, 1)
+        X(16, 4, 0) X(16, 8, 0) X(32, 8, 0) X(1, 3, 1) X(1, 7, 1) X(2, 7, 1) X(4, 7, 1) X(8, 7, 1)
 
 __host__ __device__ constexpr int bucket_make(int C, int W, int H) { return (C << 8) | (W << 1) | H; }
 __host__ __device__ constexpr int bucket_C(int id) { return id >> 8; }
@@ -773,8 +845,8 @@ __host__ __device__ constexpr int bucket_capacity(int C, int W) {
     if (N <= bucket_capacity(CC, WW)) return bucket_make(CC, WW, HH);
 __host__ __device__ __forceinline__ int bucket_id(int N, int mode = 0) {
     if (mode == 1) {
-        WX_PICK(1, 1, 0) WX_PICK(1, 3, 1) WX_PICK(1, 7, 1) WX_PICK(2, 3, 1) WX_PICK(2, 7, 1) WX_PICK(4, 7, 1)
-        WX_PICK(8, 7, 1) WX_PICK(16, 8, 0)
+        WX_PICK(1, 1, 0) WX_PICK(1, 3, 1) WX_PICK(1, 7, 1) WX_PICK(2, 7, 1) WX_PICK(4, 7, 1) WX_PICK(8, 7, 1)
+        WX_PICK(16, 8, 0)
     } else {
         WX_PICK(1, 1, 0) WX_PICK(2, 1, 0) WX_PICK(4, 1, 0) WX_PICK(6, 1, 0) WX_PICK(8, 1, 0) WX_PICK(12, 1, 0)
         WX_PICK(16, 1, 0) WX_PICK(24, 1, 0) WX_PICK(32, 1, 0) WX_PICK(16, 4, 0) WX_PICK(16, 8, 0)
@@ -809,9 +881,15 @@ struct AlignArgs {
 };
 
 
+// Latency buckets (H) claim more than half of a CU's 160 KB LDS so that the dispatcher
+// places one workgroup per CU: two 8-wave workgroups on one CU would share its SIMDs
+// (4 waves per SIMD) while other CUs idle.
+constexpr int kLatencyLdsFloats = 84 * 1024 / 4;
+
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) void align_dp_kernel(AlignArgs a) {
-    __shared__ float lds[(H ? 3 : 2) * kChunk * VS];
+__global__ __launch_bounds__(kWave*(W + H))
+    __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(AlignArgs a) {
+    __shared__ float lds[H ? kLatencyLdsFloats : 2 * kChunk * VS];
     __shared__ float c0b[H ? 2 * kChunk : 1];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
