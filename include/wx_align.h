@@ -49,7 +49,10 @@ enum {
     WX_E_LAUNCH = 1005     /* kernel launch failed */
 };
 
-#define WX_MAX_VOCAB 64      /* emission columns held in LDS per row */
+#define WX_MAX_VOCAB 16384   /* emission columns (V > 64: each segment's used columns are
+                                gathered into a compact row of at most 256) */
+#define WX_MAX_SEGMENT_COLUMNS 256 /* V > 64: distinct columns one segment may use (column 0,
+                                      the blank and its token ids) */
 #define WX_MAX_TOKENS 16000  /* tokens per segment (8 waves x 64 lanes x 32 cells, less halos) */
 
 const char* wx_version(void);
@@ -57,7 +60,7 @@ const char* wx_strerror(int code);
 
 /* get_trellis (alignment.py:359-379), batched.  trellis is CSR: segment s occupies
  * (T_s+1)*(N_s+1) floats starting at element tr_off[s] (row-major [T_s+1][N_s+1]).
- * max_N = max_s N_s (host). */
+ * max_N = max_s N_s (host).  A segment over WX_MAX_SEGMENT_COLUMNS (V > 64) is all NaN. */
 int wx_trellis(const float* em, const int64_t* em_off, int32_t V,
                const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
                int32_t S, int64_t max_N, float* trellis, const int64_t* tr_off, void* stream);
@@ -88,7 +91,9 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
  * (never materialised), argmax, backtrack and merge_repeats.  Outputs are CSR by tok_off:
  * seg_start/seg_end (frames, end exclusive) and seg_score of token k (the k-th
  * merge_repeats segment; a successful path always yields exactly N_s of them).
- * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None).
+ * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None),
+ * 2 not computed: V > 64 and the segment uses more than WX_MAX_SEGMENT_COLUMNS distinct
+ * emission columns.
  * min_N/max_N/sum_T describe the batch (host values). */
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,

@@ -59,12 +59,14 @@ def test_argument_validation_without_device(lib):
     assert lib.wx_align_dp(None, None, 32, None, None, None, 0, 0, 0, 0, None, None, None, None, None,
                            None, 0, None) == 0
     dummy = ctypes.c_void_p(8)
-    assert lib.wx_align_dp(dummy, dummy, 100, dummy, dummy, dummy, 1, 1, 1, 10, dummy, dummy, dummy, dummy,
+    assert lib.wx_align_dp(dummy, dummy, 20000, dummy, dummy, dummy, 1, 1, 1, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 1 << 30, None) == 1002
     assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 20000, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 1 << 30, None) == 1003
     assert lib.wx_align_dp(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 10, 10, dummy, dummy, dummy, dummy,
                            dummy, dummy, 16, None) == 1004
+    assert lib.wx_align_dp_mode(dummy, dummy, 32, dummy, dummy, dummy, 1, 1, 10, 10, dummy, dummy, dummy, dummy,
+                                dummy, dummy, 1 << 30, 7, None) == 1001  # unknown launch shape
     assert lib.wx_binarize(None, None, -1, None, None, None, 0.5, 0.3, 1.0, 0.0, 0.0, None, None, None, None,
                            None) == 1001
 

@@ -150,6 +150,69 @@ def test_align_dp_bucket_capacity_edges(mode):
         _check_vs_oracle(cases, f"edges V{V} mode {mode}", mode)
 
 
+def _large_vocab_cases(rng, V, n, T_range, N_range, distinct):
+    """ja/zh-like: a V-symbol vocabulary, each segment using `distinct` of its symbols."""
+    cases = []
+    for _ in range(n):
+        T = int(rng.integers(*T_range))
+        N = int(rng.integers(*N_range))
+        bl = int(rng.integers(0, V))
+        logits = rng.standard_normal((T, V)).astype(np.float32)
+        logits[:, bl] += 6.0
+        pool = rng.choice(np.array([v for v in range(V) if v != bl]), size=min(distinct, V - 1), replace=False)
+        toks = pool[rng.integers(0, len(pool), N)]
+        if N <= T - 2:
+            fr = np.sort(rng.choice(np.arange(1, T - 1), N, replace=False))
+            logits[fr, toks] += 12.0
+        em = torch.log_softmax(torch.from_numpy(logits), -1).numpy()
+        cases.append({"em": np.ascontiguousarray(em), "tokens": toks.astype(np.int64), "blank": np.int64(bl)})
+    return cases
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("V", [100, 1000, 4000])
+def test_align_dp_large_vocabulary_vs_oracle(V, mode):
+    """V > 64 (e.g. the ja/zh wav2vec2 character vocabularies): each segment's used columns
+    are gathered into a compact LDS row; up to 254 distinct tokens + blank + column 0."""
+    rng = np.random.default_rng(V + mode)
+    cases = _large_vocab_cases(rng, V, 6, (300, 900), (40, 280), 60)
+    cases += _large_vocab_cases(rng, V, 3, (700, 1500), (250, 600), min(V - 2, 250))
+    cases += _large_vocab_cases(rng, V, 2, (10, 40), (30, 60), 30)  # N > T: backtrack fails
+    _check_vs_oracle(cases, f"V{V} mode {mode}", mode)
+
+
+def test_align_dp_large_vocabulary_too_many_columns():
+    """More than 256 distinct columns in one segment: status 2 (not computed), neighbours fine."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(9)
+    ok_cases = _large_vocab_cases(rng, 1000, 2, (600, 700), (100, 200), 40)
+    big = _large_vocab_cases(rng, 1000, 1, (900, 1000), (600, 700), 400)
+    cases = [ok_cases[0], big[0], ok_cases[1]]
+    b = _batch(cases)
+    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b))
+    assert list(st) == [0, 2, 0]
+    for s_, c in ((0, cases[0]), (2, cases[2])):
+        ok, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
+        a, e = b.tok_off[s_], b.tok_off[s_ + 1]
+        assert ok and ts[s_] == tso and np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo)
+
+
+def test_trellis_large_vocabulary_vs_oracle():
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(31)
+    cases = _large_vocab_cases(rng, 500, 4, (50, 400), (5, 120), 50)
+    b = _batch(cases)
+    flat, offs = _lib.trellis(b)
+    flat = flat.cpu().numpy()
+    for s_, c in enumerate(cases):
+        T, N = c["em"].shape[0], len(c["tokens"])
+        got = flat[offs[s_]:offs[s_] + (T + 1) * (N + 1)].reshape(T + 1, N + 1)
+        exp = oracle.trellis(c["em"], c["tokens"], int(c["blank"]))
+        assert np.array_equal(got, exp, equal_nan=True), f"segment {s_}"
+
+
 def test_align_dp_config2_batch_vs_oracle():
     """BASELINE config 2: 64 x 30 s segments (T=1499, V=32, N~U[300,500])."""
     rng = np.random.default_rng(2)

@@ -20,7 +20,8 @@ LIB_PATH = os.environ.get("WX_LIB_PATH") or os.path.join(_HERE, "libwxalign.so")
 SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
-MAX_VOCAB = 64
+MAX_VOCAB = 16384
+MAX_SEGMENT_COLUMNS = 256  # V > 64: distinct emission columns one segment may use
 MAX_TOKENS = 16000
 
 _vp = ctypes.c_void_p
@@ -180,7 +181,7 @@ class Batch:
 
 def _validate(b: Batch):
     if b.V < 1 or b.V > MAX_VOCAB:
-        raise WXError(f"vocabulary size {b.V} outside [1, {MAX_VOCAB}] (compact the emission columns first)")
+        raise WXError(f"vocabulary size {b.V} outside [1, {MAX_VOCAB}]")
     if b.max_N > MAX_TOKENS:
         raise WXError(f"a segment has {b.max_N} tokens; the kernel supports up to {MAX_TOKENS}")
 

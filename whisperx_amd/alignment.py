@@ -325,6 +325,10 @@ def _run_dp(ems, toks, blanks, dev):
     se = seg_end.cpu().numpy()
     sc = seg_score.cpu().numpy()
     st = status.cpu().numpy()
+    if (st == 2).any():
+        i = int(np.flatnonzero(st == 2)[0])
+        raise _lib.WXError(f"segment {i} uses more than {_lib.MAX_SEGMENT_COLUMNS} distinct characters of the "
+                           f"{batch.V}-symbol alignment vocabulary; split it into shorter segments")
     out = []
     for i in range(batch.S):
         a, b = batch.tok_off[i], batch.tok_off[i + 1]

@@ -143,18 +143,48 @@ __device__ __forceinline__ void glds_dwordx4(const float* sbase, unsigned voff, 
                  : "memory");
 }
 
+// Large vocabularies (V > 64, e.g. ja/zh character sets): the DP reads only column 0, the
+// blank and the segment's own tokens, so a per-segment column map (built in LDS by
+// build_colmap) lets the staging gather exactly those columns into a compact LDS row of
+// VS = kGatherVS floats.  Token ids are remapped to their compact rank.
+constexpr int kGatherVS = 256;                      // compact row width (distinct columns)
+constexpr int kMaxVocabWords = WX_MAX_VOCAB / 32;   // used-column bitmap words
+
+struct ColMap {
+    const unsigned* bm;  // LDS: used-column bitmap
+    const int* wpre;     // LDS: set bits in the words before each word
+    const int* cols;     // LDS: compact index -> column
+    int n;               // compact width (uniform)
+    __device__ __forceinline__ int rank(int c) const {
+        const int w = c >> 5;
+        return wpre[w] + __popc(bm[w] & ((1u << (c & 31)) - 1u));
+    }
+};
+
 // Stage emission rows [r0, r0+nrows) of a segment into LDS buffer `dst` (row stride VS
 // floats).  Every wave of the workgroup issues its share.  When V == VS == 32 and the
 // rows are 16-byte aligned (`x4`), a chunk is one contiguous 4 KB block in both places:
-// one 16-byte-per-lane instruction moves 8 rows.  Otherwise one dword per lane per row,
-// lanes >= V masked.  Asynchronous: every wave waits vmcnt(0) before the chunk barrier.
+// one 16-byte-per-lane instruction moves 8 rows.  VS == kGatherVS: per row, lane l of pass
+// i gathers column cols[64i + l] (the LDS-DMA source address is per lane, the destination
+// lane-linear).  Otherwise one dword per lane per row, lanes >= V masked.  Asynchronous:
+// every wave waits vmcnt(0) before the chunk barrier.
 template <int VS, int W, bool ONE_WAVE = false>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, int r0, int nrows, float* dst,
-                                           bool x4) {
+                                           bool x4, const ColMap& cm) {
     const int wv = ONE_WAVE ? 0 : uniform((int)threadIdx.x >> 6);
     const int l = lane_id();
     const unsigned base = (unsigned)uniform((int)lds_addr(dst));
-    if (VS == 32 && x4) {
+    if (VS == kGatherVS) {
+        const int passes = (cm.n + kWave - 1) / kWave;
+        for (int i = 0; i < passes; ++i) {
+            const int c = i * kWave + l;
+            if (c < cm.n) {
+                const unsigned off = (unsigned)cm.cols[c] * 4u;
+                for (int r = wv; r < nrows; r += W)
+                    glds_dword(E + (int64_t)(r0 + r) * V, off, base + (unsigned)(r * VS * 4 + i * kWave * 4));
+            }
+        }
+    } else if (VS == 32 && x4) {
         for (int i = wv; i * 8 < nrows; i += W) {
             if (i * 8 + (l >> 3) < nrows)
                 glds_dwordx4(E + (int64_t)(r0 + i * 8) * 32, (unsigned)l * 16u, base + (unsigned)(i * 1024));
@@ -168,6 +198,57 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, i
 #endif
         }
     }
+}
+
+// The column map of one segment (all threads of the workgroup): columns 0 and `blank` and
+// every token id (ids outside [0, V) count as 0, as the DP reads them).  Returns the compact
+// width, uniform; > kGatherVS means the segment cannot be staged.
+__device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, int V, unsigned* bm, int* wpre,
+                            int* cols) {
+    const int nw = (V + 31) >> 5;
+    for (int w = (int)threadIdx.x; w < nw; w += (int)blockDim.x) bm[w] = 0u;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int b = (blank >= 0 && blank < V) ? blank : 0;
+        atomicOr(&bm[0], 1u);
+        atomicOr(&bm[b >> 5], 1u << (b & 31));
+    }
+    for (int j = (int)threadIdx.x; j < N; j += (int)blockDim.x) {
+        int t = tok[j];
+        t = (t >= 0 && t < V) ? t : 0;
+        atomicOr(&bm[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < kWave) {  // exclusive prefix of popcounts, 64 words per pass
+        int base = 0;
+        for (int w0 = 0; w0 < nw; w0 += kWave) {
+            const int w = w0 + (int)threadIdx.x;
+            const int c = w < nw ? __popc(bm[w]) : 0;
+            int incl = c;
+#pragma unroll
+            for (int off = 1; off < kWave; off <<= 1) {
+                const int y = __shfl_up(incl, off);
+                if ((int)threadIdx.x >= off) incl += y;
+            }
+            if (w < nw) wpre[w] = base + incl - c;
+            base += __shfl(incl, kWave - 1);
+        }
+        if (threadIdx.x == 0) wpre[nw] = base;
+    }
+    __syncthreads();
+    const int n = wpre[nw];
+    if (n <= kGatherVS) {
+        for (int w = (int)threadIdx.x; w < nw; w += (int)blockDim.x) {
+            unsigned m = bm[w];
+            int k = wpre[w];
+            while (m) {
+                cols[k++] = w * 32 + __ffs((int)m) - 1;
+                m &= m - 1u;
+            }
+        }
+    }
+    __syncthreads();
+    return uniform(n);
 }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -303,12 +384,13 @@ struct Forward {
                                                float* __restrict__ tr,        // MODE 1: trellis
                                                float* lds /* kBufs * kChunk * VS */,
                                                float* c0b /* H: 2 * kChunk column-0 values */,
-                                               float* xh /* 2 * W * 64: chunk halo copies */, bool x4) {
+                                               float* xh /* 2 * W * 64: chunk halo copies */, bool x4,
+                                               const ColMap& cm /* VS == kGatherVS: column map */) {
         const int wv = uniform((int)threadIdx.x >> 6);
         const int T = d.T, N = d.N;
         const int nch = (T + kChunk - 1) / kChunk;
         if (H && wv == W) {
-            helper(d, E, V, lds, c0b, nch, x4);
+            helper(d, E, V, lds, c0b, nch, x4, cm);
             return;
         }
         const int l = lane_id();
@@ -320,13 +402,13 @@ struct Forward {
         if (W > 1 && wv > 0 && Geo::lane_of(wv, Geo::HL) >= L.G) {
             // no column of this wave exists: keep the barrier count (and, without a helper,
             // this wave's share of the staging)
-            if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4);
+            if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
             for (int q = 0; q < nch; ++q) {
                 wait_vm();
                 __syncthreads();
                 if (!H && q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
-                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4);
+                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4, cm);
             }
             return;
         }
@@ -341,9 +423,9 @@ struct Forward {
             const int j = f + k;
             int tk = (k < cnt && j <= N) ? tok[d.tok0 + j - 1] : 0;
             tk = (tk >= 0 && tk < V) ? tk : 0;
-            toff[k] = tk * 4;
+            toff[k] = (VS == kGatherVS ? cm.rank(tk) : tk) * 4;
         }
-        const int boff = d.blank * 4;
+        const int boff = (VS == kGatherVS ? cm.rank(d.blank) : d.blank) * 4;  // column 0 has rank 0
         // column N = slot C-1 of useful lane G-1
         int own_w, own_l;
         Geo::owner(L.G - 1, own_w, own_l);
@@ -359,7 +441,7 @@ struct Forward {
         st.t = 0;
         const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
 
-        if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4);
+        if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
 #ifdef WX_PHASE_TIMING
         unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0;
 #endif
@@ -383,7 +465,7 @@ struct Forward {
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
-                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4);
+                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4, cm);
                 if (MODE == 0 && wv == 0 && l < rows) q0[q * kChunk + l] = exp_cr(buf[l * VS]);  // never idle
             }
             const char* bb = reinterpret_cast<const char*>(buf);
@@ -422,12 +504,12 @@ struct Forward {
     // q+1 are staged and column 0 of chunk q is in c0b[q & 1].  (q0 is filled after the
     // forward pass, while wave 0 walks: fill_q0.)
     __device__ static void helper(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* c0b,
-                                  int nch, bool x4) {
+                                  int nch, bool x4, const ColMap& cm) {
         const int T = d.T, N = d.N;
         const int inf_from = T + 1 - N;
         double acc = 0.0;  // sum of em[0..t-1, 0], uniform
-        if (nch > 0) stage_rows<VS, 1, true>(E, V, 0, min(kChunk, T), lds, x4);
-        if (nch > 1) stage_rows<VS, 1, true>(E, V, kChunk, min(kChunk, T - kChunk), lds + kChunk * VS, x4);
+        if (nch > 0) stage_rows<VS, 1, true>(E, V, 0, min(kChunk, T), lds, x4, cm);
+        if (nch > 1) stage_rows<VS, 1, true>(E, V, kChunk, min(kChunk, T - kChunk), lds + kChunk * VS, x4, cm);
         wait_vm();
         column0(0, T, inf_from, lds, c0b, acc);
 #ifdef WX_PHASE_TIMING
@@ -441,7 +523,7 @@ struct Forward {
             WX_T(h2);
             if (q + 2 < nch)
                 stage_rows<VS, 1, true>(E, V, (q + 2) * kChunk, min(kChunk, T - (q + 2) * kChunk),
-                                        lds + ((q + 2) % kBufs) * kChunk * VS, x4);
+                                        lds + ((q + 2) % kBufs) * kChunk * VS, x4, cm);
             WX_T(h3);
             if (q + 1 < nch) column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
             WX_T(h4);
@@ -886,14 +968,40 @@ struct AlignArgs {
 // (4 waves per SIMD) while other CUs idle.
 constexpr int kLatencyLdsFloats = 84 * 1024 / 4;
 
+// Column-map LDS of the gather (large-vocabulary) instantiations.
+template <int VS>
+struct ColMapLds {
+    static constexpr bool kOn = VS == kGatherVS;
+    unsigned bm[kOn ? kMaxVocabWords : 1];
+    int wpre[kOn ? kMaxVocabWords + 1 : 1];
+    int cols[kOn ? kGatherVS : 1];
+};
+
+// Build the segment's column map when VS is the gather width; returns false (and the
+// caller stops) when the segment uses more distinct columns than a compact row holds.
+template <int VS>
+__device__ __forceinline__ bool prepare_colmap(ColMapLds<VS>& m, ColMap& cm, const int32_t* tok, int N, int blank,
+                                               int V) {
+    cm.bm = m.bm;
+    cm.wpre = m.wpre;
+    cm.cols = m.cols;
+    cm.n = 0;
+    if (!ColMapLds<VS>::kOn) return true;
+    cm.n = build_colmap(tok, N, blank, V, m.bm, m.wpre, m.cols);
+    return cm.n <= kGatherVS;
+}
+
 template <int C, int VS, int W, int H>
 __global__ __launch_bounds__(kWave*(W + H))
     __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(AlignArgs a) {
-    __shared__ float lds[H ? kLatencyLdsFloats : 2 * kChunk * VS];
+    constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 3 * kChunk * VS ? kLatencyLdsFloats : 3 * kChunk * VS)
+                                 : 2 * kChunk * VS;
+    __shared__ float lds[kLdsFloats];
     __shared__ float c0b[H ? 2 * kChunk : 1];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[2];
+    __shared__ ColMapLds<VS> cml;
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     if (bucket_id(d.N, a.mode) != bucket_make(C, W, H)) return;  // another instantiation owns it
@@ -905,13 +1013,21 @@ __global__ __launch_bounds__(kWave*(W + H))
         }
         return;
     }
+    ColMap cm;
+    if (!prepare_colmap(cml, cm, a.tok + d.tok0, d.N, d.blank, a.V)) {
+        if (lane == 0) {
+            a.t_start[seg] = 0;
+            a.status[seg] = 2;  // more than kGatherVS distinct columns in one segment
+        }
+        return;
+    }
     const float* E = a.em + d.row0 * a.V;
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
     float* cn = a.cn + ((d.row0 + 4 * (int64_t)seg) & ~(int64_t)3);
     WX_STAMP_RT(4);
     WX_STAMP(0);
-    Forward<C, VS, 0, W, H != 0>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0);
+    Forward<C, VS, 0, W, H != 0>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm);
     WX_STAMP(1);
     wait_vm();
     block_fence();
@@ -960,6 +1076,7 @@ template <int C, int VS, int W>
 __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
     __shared__ float lds[2 * kChunk * VS];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
+    __shared__ ColMapLds<VS> cml;
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     if (bucket_id(d.N) != bucket_make(C, W, 0)) return;
@@ -969,8 +1086,15 @@ __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
         for (int t = lane; t <= d.T; t += kWave * W) tr[t] = INFINITY;
         return;
     }
+    ColMap cm;
+    if (!prepare_colmap(cml, cm, a.tok + d.tok0, d.N, d.blank, a.V)) {  // too many distinct columns
+        const int64_t n = (int64_t)(d.T + 1) * (d.N + 1);
+        for (int64_t i = lane; i < n; i += kWave * W) tr[i] = NAN;
+        return;
+    }
     const float* E = a.em + d.row0 * a.V;
-    Forward<C, VS, 1, W, false>::run(d, E, a.V, a.tok, nullptr, nullptr, nullptr, tr, lds, nullptr, xh, a.x4 != 0);
+    Forward<C, VS, 1, W, false>::run(d, E, a.V, a.tok, nullptr, nullptr, nullptr, tr, lds, nullptr, xh, a.x4 != 0,
+                                     cm);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1470,7 +1594,7 @@ const char* wx_strerror(int code) {
     switch (code) {
         case WX_OK: return "ok";
         case WX_E_INVALID: return "invalid argument";
-        case WX_E_VOCAB: return "vocabulary size outside [1, 64]";
+        case WX_E_VOCAB: return "vocabulary size outside [1, 16384]";
         case WX_E_TOO_LONG: return "segment has more than 16000 tokens";
         case WX_E_WORKSPACE: return "workspace too small";
         case WX_E_LAUNCH: return "kernel launch failed";
@@ -1541,7 +1665,8 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
         if (ids[i] == bucket_make(CC, WW, HH)) {                                                       \
             const dim3 block(kWave * (WW + HH));                                                       \
             if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW, HH>), grid, block, 0, s, a);   \
-            else hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW, HH>), grid, block, 0, s, a);           \
+            else if (V <= 64) hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW, HH>), grid, block, 0, s, a); \
+            else hipLaunchKernelGGL((align_dp_kernel<CC, kGatherVS, WW, HH>), grid, block, 0, s, a);    \
         }
         WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
@@ -1568,7 +1693,8 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
 #define WX_LAUNCH_TR(CC, WW, HH)                                                                        \
         if (!HH && ids[i] == bucket_make(CC, WW, 0)) {                                                \
             if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
-            else hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a);         \
+            else if (V <= 64) hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a); \
+            else hipLaunchKernelGGL((trellis_kernel<CC, kGatherVS, WW>), grid, dim3(kWave * WW), 0, s, a); \
         }
         WX_BUCKETS(WX_LAUNCH_TR)
 #undef WX_LAUNCH_TR
