@@ -282,6 +282,22 @@ def main():
                                   "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b2.Ts, b2.Ns))) / (d2 / 5)}
             del p2, b2
             torch.cuda.empty_cache()
+            # the north star's roofline case: T=3000 x V=32 trellises (N ~ 900, 60 s segments)
+            rng3 = np.random.default_rng(78)
+            n3 = 2048
+            ems3, toks3 = make_batch(rng3, n3, 2999, V, 850, 951, device)
+            b3 = _lib.Batch(ems3, toks3, [0] * n3, device=device)
+            del ems3
+            p3 = _lib.AlignPlan(b3)
+            h3, d3 = time_steps(p3, 3, 1, False)
+            B3 = algorithmic_bytes(b3.Ts, b3.Ns, V)
+            extra["saturated_T3000"] = {"segments": n3, "ms_per_step": 1000 * d3 / 3,
+                                        "audio_sec_per_s": sum(b3.Ts) * FRAME_S / (d3 / 3),
+                                        "achieved_GBps": B3 / (d3 / 3) / 1e9,
+                                        "frac": B3 / (d3 / 3) / 1e9 / HBM_PEAK_GBPS,
+                                        "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b3.Ts, b3.Ns))) / (d3 / 3)}
+            del p3, b3
+            torch.cuda.empty_cache()
         if not args.no_cpu and world == 1:
             ems_cpu = [e.cpu() for e in ems]
             out["cpu_baseline"] = cpu_port_baseline(ems_cpu, toks)

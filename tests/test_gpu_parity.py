@@ -127,7 +127,7 @@ def _capacity(C, W):
     return C * (64 + (W - 1) * (64 - ((32 + C - 1) // C if W > 1 else 0)))
 
 
-THROUGHPUT_BUCKETS = [(1, 1), (2, 1), (4, 1), (6, 1), (8, 1), (12, 1), (16, 1), (24, 1), (32, 1), (16, 4), (16, 8)]
+THROUGHPUT_BUCKETS = [(1, 1), (2, 1), (4, 1), (6, 1), (8, 1), (8, 2), (8, 4), (8, 8), (16, 8)]
 LATENCY_BUCKETS = [(1, 1), (1, 3), (1, 7), (2, 7), (4, 7), (8, 7), (16, 8)]
 
 

@@ -363,6 +363,10 @@ struct Forward {
     static constexpr int kRowBytes = VS * 4;
     static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves)
     static constexpr int kBufs = H ? 3 : 2;   // emission chunk buffers in LDS
+    // Software-pipelined LDS operands where the extra registers keep the occupancy that
+    // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
+    // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
+    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
     using Geo = Geometry<C, W>;
     static_assert(!(H && MODE == 1), "the materialising kernel computes column 0 in wave 0");
 
@@ -575,9 +579,15 @@ struct Forward {
                                                  int cnt, bool owner, int N, float* __restrict__ cn,
                                                  float* __restrict__ tr) {
         constexpr int kColLds = 3, kColFinite = 1, kColAny = 2;
-        if (H && rows == kChunk) {  // latency buckets: software-pipelined full chunk
-            pipelined_chunk<WAVE0 ? kColLds : 0>(bb, c0q, toff, boff, st, WAVE0 && is_short, halo, f, cnt, owner, N,
-                                                 cn, tr);
+        if (kPipelined && rows == kChunk) {  // software-pipelined full chunk
+            if (!WAVE0)
+                pipelined_chunk<0>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
+            else if (H)
+                pipelined_chunk<kColLds>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+            else if (st.t + kChunk < inf_from)
+                pipelined_chunk<kColFinite>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+            else
+                pipelined_chunk<kColAny>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             return;
         }
         int r = 0;
@@ -627,9 +637,9 @@ struct Forward {
     // returns in order.
     template <int COL>
     __device__ __forceinline__ static void pipelined_chunk(const char* bb, const float* c0q, const int (&toff)[C],
-                                                           int boff, State& st, bool is_short, bool halo, int f,
-                                                           int cnt, bool owner, int N, float* __restrict__ cn,
-                                                           float* __restrict__ tr) {
+                                                           int boff, State& st, int inf_from, bool is_short,
+                                                           bool halo, int f, int cnt, bool owner, int N,
+                                                           float* __restrict__ cn, float* __restrict__ tr) {
         const char* ga[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) ga[k] = bb + toff[k];
@@ -644,7 +654,7 @@ struct Forward {
                 load_row<COL>(bb, ga, (u + 3) * kRowBytes, boff, c0q + u + 3, rw[u + 3]);
             }
             __builtin_amdgcn_sched_barrier(0);
-            advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, 0x7fffffff, is_short, halo, f, cnt, N, tr);
+            advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
             hist[u & (kUnroll - 1)] = st.cur[C - 1];
             ++st.t;
             if (MODE == 0 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
@@ -680,6 +690,7 @@ struct Forward {
 #pragma unroll
         for (int k = 0; k < C; ++k) rw.et[k] = *reinterpret_cast<const float*>(ga[k] + ro);
         if (COL == 3) rw.c0 = *c0;
+        if (COL == 1 || COL == 2) rw.c0 = *reinterpret_cast<const float*>(gb + ro);  // em[t, 0]
     }
 
     template <int COL>
@@ -700,7 +711,7 @@ struct Forward {
             st.cur[k] = nan_max(s, c);
         }
         if (COL == 1 || COL == 2) {
-            const float e0 = *reinterpret_cast<const float*>(gb + ro);
+            const float e0 = rw.c0;
             st.acc += (double)e0;
             st.col0 = (COL == 1 || st.t + 1 < inf_from) ? (float)st.acc : INFINITY;
         }
@@ -881,7 +892,15 @@ __device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* 
         int tk = tok[k];
         tk = (tk >= 0 && tk < V) ? tk : 0;
         double sum = (double)exp_cr(E[(int64_t)s * V + tk]);
-        for (int x = s + 1; x < e; ++x) sum += (double)q0[x];
+        int x = s + 1;
+        for (; x + 8 <= e; x += 8) {  // 8 loads in flight, adds in the reference's order
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = q0[x + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum += (double)v[u];
+        }
+        for (; x < e; ++x) sum += (double)q0[x];
         seg_end[k] = e;
         seg_score[k] = sum / (double)(e - s);
     }
@@ -903,15 +922,17 @@ __device__ __forceinline__ void block_fence() {
 
 // (cells per lane C, DP waves per segment W, helper wave H) buckets, one kernel
 // instantiation each; id = C << 8 | W << 1 | H.
-// Throughput mode (many segments in flight): one wave per segment up to N = 2048; longer
-// transcripts use W waves with a chunk halo (Geometry).  Latency mode (few segments: the
+// Throughput mode (many segments in flight): one wave per segment up to N = 512; longer
+// transcripts use W waves of 8 cells per lane with a chunk halo (Geometry): at most ~124
+// VGPRs keeps 4 waves per SIMD, which beat one wide (16-32 cells per lane) wave per
+// segment by 4-10% on T = 3000, N = 900 batches.  Latency mode (few segments: the
 // chip would otherwise be mostly idle): a segment's columns are spread over 3 or 7 waves
 // plus the helper (at most 2 waves per SIMD, which still issue at the full rate), so each
 // wave issues fewer instructions per time step.  (Waves beyond column N only keep the
 // barrier count, so a wide bucket costs no time: 30 s segments, N 257..704, share one.)
-#define WX_BUCKETS(X)                                                                                         \
-    X(1, 1, 0) X(2, 1, 0) X(4, 1, 0) X(6, 1, 0) X(8, 1, 0) X(12, 1, 0) X(16, 1, 0) X(24, 1, 0) X(32, 1, 0)    \
-        X(16, 4, 0) X(16, 8, 0) X(32, 8, 0) X(1, 3, 1) X(1, 7, 1) X(2, 7, 1) X(4, 7, 1) X(8, 7, 1)
+#define WX_BUCKETS(X)                                                                                    \
+    X(1, 1, 0) X(2, 1, 0) X(4, 1, 0) X(6, 1, 0) X(8, 1, 0) X(8, 2, 0) X(8, 4, 0) X(8, 8, 0) X(16, 8, 0) \
+        X(32, 8, 0) X(1, 3, 1) X(1, 7, 1) X(2, 7, 1) X(4, 7, 1) X(8, 7, 1)
 
 __host__ __device__ constexpr int bucket_make(int C, int W, int H) { return (C << 8) | (W << 1) | H; }
 __host__ __device__ constexpr int bucket_C(int id) { return id >> 8; }
@@ -930,8 +951,8 @@ __host__ __device__ __forceinline__ int bucket_id(int N, int mode = 0) {
         WX_PICK(1, 1, 0) WX_PICK(1, 3, 1) WX_PICK(1, 7, 1) WX_PICK(2, 7, 1) WX_PICK(4, 7, 1) WX_PICK(8, 7, 1)
         WX_PICK(16, 8, 0)
     } else {
-        WX_PICK(1, 1, 0) WX_PICK(2, 1, 0) WX_PICK(4, 1, 0) WX_PICK(6, 1, 0) WX_PICK(8, 1, 0) WX_PICK(12, 1, 0)
-        WX_PICK(16, 1, 0) WX_PICK(24, 1, 0) WX_PICK(32, 1, 0) WX_PICK(16, 4, 0) WX_PICK(16, 8, 0)
+        WX_PICK(1, 1, 0) WX_PICK(2, 1, 0) WX_PICK(4, 1, 0) WX_PICK(6, 1, 0) WX_PICK(8, 1, 0) WX_PICK(8, 2, 0)
+        WX_PICK(8, 4, 0) WX_PICK(8, 8, 0) WX_PICK(16, 8, 0)
     }
     return bucket_make(32, 8, 0);
 }
