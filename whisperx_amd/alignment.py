@@ -205,6 +205,36 @@ def _emission(model, model_type, waveform_segment, device):
     return emissions[0].detach()
 
 
+_EMISSION_STREAMS = {}
+
+
+def _emissions(model, model_type, waveforms, device, n_streams: int = 4):
+    """_emission for every segment, one unpadded forward each (padding would change
+    wav2vec2's logits), issued round-robin on `n_streams` HIP streams: one 30 s forward's
+    GEMMs (1,499 rows) fill a fraction of the GPU, so consecutive segments overlap.  Same
+    kernels per segment as one-at-a-time; joined back onto the current stream."""
+    dev = torch.device(device) if not isinstance(device, torch.device) else device
+    if dev.type != "cuda" or n_streams <= 1 or len(waveforms) <= 1:
+        return [_emission(model, model_type, w, device) for w in waveforms]
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), n_streams)
+    streams = _EMISSION_STREAMS.get(key)
+    if streams is None:
+        streams = [torch.cuda.Stream(device=dev) for _ in range(n_streams)]
+        _EMISSION_STREAMS[key] = streams
+    main = torch.cuda.current_stream(dev)
+    out = []
+    for i, w in enumerate(waveforms):
+        st = streams[i % n_streams]
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            em = _emission(model, model_type, w, device)
+        em.record_stream(main)
+        out.append(em)
+    for st in streams:
+        main.wait_stream(st)
+    return out
+
+
 def _dp_device(device):
     """Device on which the DP runs: the model's device if it is a HIP device, else GPU 0."""
     d = torch.device(device) if not isinstance(device, torch.device) else device
@@ -276,12 +306,12 @@ def align(
         f1 = int(t1 * SAMPLE_RATE)
         f2 = int(t2 * SAMPLE_RATE)
         waveform_segment = audio[:, f1:f2]
-        em = _emission(model, model_type, waveform_segment, device)
         plan.append(("dp", len(ems)))
-        ems.append(em)
+        ems.append(waveform_segment)
         toks.append(tokens)
         blanks.append(blank_id)
         meta.append((text_clean, waveform_segment.size(0)))
+    ems = _emissions(model, model_type, ems, device)
 
     # 2b. one fused DP launch for all segments
     results = _run_dp(ems, toks, blanks, dp_dev) if ems else []

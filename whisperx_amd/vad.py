@@ -97,7 +97,7 @@ except Exception:  # stand-ins with pyannote.core semantics
             return len(self._tracks)
 
         def get_timeline(self):
-            return sorted({s for (s, _t) in self._tracks})
+            return sorted({s for (s, _t) in self._tracks}, key=Segment._key)
 
         def itertracks(self, yield_label: bool = False):
             for (s, t) in sorted(self._tracks, key=lambda st: (st[0].start, st[0].end, str(st[1]))):
