@@ -213,6 +213,21 @@ def test_trellis_large_vocabulary_vs_oracle():
         assert np.array_equal(got, exp, equal_nan=True), f"segment {s_}"
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_align_dp_long_segments_and_chunk_edges(mode):
+    """T > 8192 (walk change masks in global memory instead of LDS), T at multiples of the
+    32-row chunk and one off, T < 32, N = 1 and N = T - 1."""
+    rng = np.random.default_rng(55 + mode)
+    cases = _random_cases(rng, 2, (9000, 9400), (1200, 1800), 32, blank=0)
+    cases += _random_cases(rng, 1, (40, 41), (1, 2), 32)    # N = 1
+    cases += _random_cases(rng, 1, (90, 91), (89, 90), 32)  # N = T - 1
+    _check_vs_oracle(cases, f"long mode {mode}", mode)
+    edges = []
+    for T in (31, 32, 33, 63, 64, 65, 1023, 1024, 1025):
+        edges += _random_cases(rng, 1, (T, T + 1), (max(1, T // 4), max(2, T // 3)), 29)
+    _check_vs_oracle(edges, f"chunk edges mode {mode}", mode)
+
+
 def test_align_dp_config2_batch_vs_oracle():
     """BASELINE config 2: 64 x 30 s segments (T=1499, V=32, N~U[300,500])."""
     rng = np.random.default_rng(2)
