@@ -213,6 +213,35 @@ def test_trellis_large_vocabulary_vs_oracle():
         assert np.array_equal(got, exp, equal_nan=True), f"segment {s_}"
 
 
+@pytest.mark.parametrize("V", [32, 29])
+def test_trellis_every_bucket_vs_oracle(V):
+    """get_trellis over every launch bucket (N at each capacity and one past it, short
+    lanes, multi-wave chunk halos), T spanning several 32-row chunks: bit-exact rows (the
+    row stores go through the LDS transpose)."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(300 + V)
+    Ns = {1, 2, 3, 5, 63, 64, 65, 100}
+    for C, W in THROUGHPUT_BUCKETS:
+        cap = _capacity(C, W)
+        if cap <= 4001:
+            Ns.update({cap, cap + 1, cap - 7})
+    cases = []
+    for N in sorted(Ns):
+        T = N + int(rng.integers(2, 90)) if N > 60 else int(rng.integers(N + 2, 140))
+        cases += _random_cases(rng, 1, (T, T + 1), (N, N + 1), V)
+    cases += _random_cases(rng, 3, (5, 40), (20, 60), V)  # N > T
+    cases += _random_cases(rng, 3, (20, 300), (1, 60), V, quant=16)  # exact ties
+    b = _batch(cases)
+    flat, offs = _lib.trellis(b)
+    flat = flat.cpu().numpy()
+    for s_, c in enumerate(cases):
+        T, N = c["em"].shape[0], len(c["tokens"])
+        got = flat[offs[s_]:offs[s_] + (T + 1) * (N + 1)].reshape(T + 1, N + 1)
+        exp = oracle.trellis(c["em"], c["tokens"], int(c["blank"]))
+        assert np.array_equal(got, exp, equal_nan=True), f"V{V} segment {s_} (T={T}, N={N})"
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_align_dp_long_segments_and_chunk_edges(mode):
     """T > 8192 (walk change masks in global memory instead of LDS), T at multiples of the

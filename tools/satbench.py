@@ -1,0 +1,171 @@
+#!/usr/bin/env python
+"""Kernel A/B harness for wx_align_dp (development tool, not the bench contract).
+
+Times the fused DP on three shapes — the config-2 batch (64 x T=1499, latency shape), a
+saturated T=1499 batch and the north star's T=3000 x V=32 batch — for one or more builds of
+libwxalign.so, and checks every build's outputs against the first build's (bit-exact).
+
+    python tools/satbench.py [--libs a.so,b.so] [--cases b64,sat1499,sat3000] [--steps K]
+
+Each build runs in its own subprocess (the library path is fixed at import).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = {  # name: (segments, T, N range)
+    "b64": (64, 1499, (300, 500)),
+    "sat1499": (4096, 1499, (300, 500)),
+    "sat3000": (2048, 2999, (850, 951)),
+    "sat3000_1024": (1024, 2999, (850, 951)),
+    "sat3000_1536": (1536, 2999, (850, 951)),
+    "sat3000_1792": (1792, 2999, (850, 951)),
+    "sat3000_4096": (4096, 2999, (850, 951)),
+}
+
+
+def make_batch(S, T, V, n_lo, n_hi, seed, device):
+    import numpy as np
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    logits = torch.randn((S, T, V), generator=g, device=device)
+    logits[:, :, 0] += 6.0
+    toks = []
+    for s in range(S):
+        N = int(rng.integers(n_lo, n_hi + 1))
+        tk = rng.integers(1, V, N)
+        fr = np.sort(rng.choice(np.arange(1, T - 1), N, replace=False))
+        logits[s, torch.from_numpy(fr).to(device), torch.from_numpy(tk).to(device)] += 12.0
+        toks.append(tk.tolist())
+    em = torch.log_softmax(logits, -1)
+    return [em[s] for s in range(S)], toks
+
+
+def child(args):
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, ROOT)
+    from whisperx_amd import _lib
+
+    dev = torch.device("cuda", 0)
+    out = {}
+    for case in args.cases.split(","):
+        if case.startswith("tr"):  # materialised trellis (wx_trellis): HBM-write-bound
+            S, T, (lo, hi) = CASES[case[2:]]
+            ems, toks = make_batch(S, T, 32, lo, hi, 1234, dev)
+            b = _lib.Batch(ems, toks, [0] * S, device=dev)
+            del ems
+            tr, offs = _lib.trellis(b)
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(args.steps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                _lib.load().wx_trellis(_lib._ptr(b.em), _lib._ptr(b.em_off_d), b.V, _lib._ptr(b.tok),
+                                       _lib._ptr(b.tok_off_d), _lib._ptr(b.blank), b.S, b.max_N, _lib._ptr(tr),
+                                       _lib._ptr(_lib._dev_i64(offs, dev)), _lib._stream(dev))
+                e1.record()
+                torch.cuda.synchronize()
+                ms.append(e0.elapsed_time(e1))
+            med = float(np.median(ms))
+            Bytes = sum(4 * t * 32 + 4 * n + 4 * (t + 1) * (n + 1) for t, n in zip(b.Ts, b.Ns))
+            cells = float(sum(t * n for t, n in zip(b.Ts, b.Ns)))
+            digest = [int(np.int64(hash(tr[: min(tr.numel(), 1 << 24)].cpu().numpy().tobytes()) & 0x7FFFFFFF))]
+            out[case] = {"ms_med": med, "ms_min": float(min(ms)), "cells_per_s": cells / (med / 1e3),
+                         "GBps": Bytes / (med / 1e3) / 1e9, "frac": Bytes / (med / 1e3) / 8e12, "digest": digest}
+            del tr, b
+            torch.cuda.empty_cache()
+            continue
+        S, T, (lo, hi) = CASES[case]
+        ems, toks = make_batch(S, T, 32, lo, hi, 1234, dev)
+        b = _lib.Batch(ems, toks, [0] * S, device=dev)
+        del ems
+        p = _lib.AlignPlan(b, mode=args.mode)
+        for _ in range(2):
+            p.run()
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for a, e in ev:
+            a.record(st)
+            p.run()
+            e.record(st)
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(e) for a, e in ev]
+        cells = float(sum(t * n for t, n in zip(b.Ts, b.Ns)))
+        Bytes = sum(4 * t * 32 + 4 * n + (t * n) // 8 + 16 * n for t, n in zip(b.Ts, b.Ns))
+        med = float(np.median(ms))
+        res = [x.cpu().numpy() for x in p.run()]
+        torch.cuda.synchronize()
+        digest = [int(np.int64(hash(r.tobytes()) & 0x7FFFFFFF)) for r in res]
+        out[case] = {"ms_med": med, "ms_min": float(min(ms)), "cells_per_s": cells / (med / 1e3),
+                     "GBps": Bytes / (med / 1e3) / 1e9, "frac": Bytes / (med / 1e3) / 8e12, "digest": digest}
+        if args.phases:
+            import ctypes
+            lib = _lib.load()
+            n = min(S, 8192)
+            buf = (ctypes.c_ulonglong * (6 * n))()
+            lib.wx_debug_phases(buf, n)
+            ph = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)
+            fwd, walk, mrg = ph[:, 1] - ph[:, 0], ph[:, 2] - ph[:, 1], ph[:, 3] - ph[:, 2]
+            out[case]["phases_cyc_med"] = {"forward": float(np.median(fwd)), "walk": float(np.median(walk)),
+                                           "merge": float(np.median(mrg)), "per_step_fwd": float(np.median(fwd)) / T,
+                                           "per_step_walk": float(np.median(walk)) / T,
+                                           "walk_max": float(walk.max()), "fwd_max": float(fwd.max())}
+            rt = (ph[:, 5] - ph[:, 4]) / 100.0  # s_memrealtime ticks at 100 MHz -> us
+            out[case]["seg_us_med"] = float(np.median(rt))
+            ent = (ph[:, 4] - ph[:, 4].min()) / 100.0
+            out[case]["entry_us_q"] = [float(np.quantile(ent, q)) for q in (0.1, 0.5, 0.75, 0.9, 0.99, 1.0)]
+            out[case]["clock_GHz"] = float(np.median((ph[:, 3] - ph[:, 0]) / np.maximum(rt, 1e-9) / 1e3))
+        del p, b
+        torch.cuda.empty_cache()
+    print("RESULT " + json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default=os.path.join(ROOT, "whisperx_amd", "libwxalign.so"))
+    ap.add_argument("--cases", default="b64,sat1499,sat3000")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--mode", type=int, default=-1)
+    ap.add_argument("--child", action="store_true")
+    ap.add_argument("--phases", action="store_true", help="library built with -DWX_PHASE_TIMING")
+    args = ap.parse_args()
+    if args.child:
+        child(args)
+        return
+    results = {}
+    for lib in args.libs.split(","):
+        env = dict(os.environ, WX_LIB_PATH=os.path.abspath(lib), PYTHONHASHSEED="0")
+        t0 = time.time()
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--cases", args.cases,
+                            "--steps", str(args.steps), "--mode", str(args.mode)] + (["--phases"] if args.phases else []),
+                           env=env, capture_output=True, text=True, timeout=600)
+        line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+        if r.returncode != 0 or not line:
+            print(f"{lib}: FAILED rc={r.returncode}\n{r.stderr[-3000:]}", flush=True)
+            sys.exit(1)
+        results[lib] = json.loads(line[0][7:])
+        print(f"{os.path.basename(lib)} ({time.time() - t0:.0f}s):", flush=True)
+        for case, v in results[lib].items():
+            print(f"  {case:9s} {v['ms_med']:9.4f} ms  {v['cells_per_s']:.3e} cells/s  frac {v['frac']:.3f}", flush=True)
+            if "phases_cyc_med" in v:
+                print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
+    libs = list(results)
+    for lib in libs[1:]:
+        for case in results[lib]:
+            if results[lib][case]["digest"] != results[libs[0]][case]["digest"]:
+                print(f"MISMATCH {lib} {case} vs {libs[0]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

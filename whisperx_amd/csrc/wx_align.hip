@@ -47,6 +47,9 @@ namespace wx {
 constexpr int kWave = 64;
 constexpr int kChunk = 32;  // emission rows per LDS buffer == bits per column word
 constexpr int kUnroll = 8;  // time steps per unrolled group
+#ifndef WX_C8_UNROLL
+#define WX_C8_UNROLL 8  // ... for C >= 8 non-pipelined waves (Forward::kU; 4: A/B neutral)
+#endif
 constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
 __device__ __forceinline__ float nan_max(float a, float b) {
@@ -368,6 +371,9 @@ struct Forward {
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
     static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
     using Geo = Geometry<C, W>;
+    // Steps per unrolled group of the non-pipelined chunk (hipcc hoists the group's LDS
+    // loads; a multiple of 4: column-N history is stored as float4).
+    static constexpr int kU = C >= 8 ? WX_C8_UNROLL : kUnroll;
     static_assert(!(H && MODE == 1), "the materialising kernel computes column 0 in wave 0");
 
     // Per-lane state of the forward pass.
@@ -377,6 +383,12 @@ struct Forward {
         double acc;   // W == 1 / !H: column-0 cumsum (fp64)
         float col0;   // tr[t][0] for the current step (column-1 wave)
         int t;
+        // MODE 1 row stores, transposed through LDS so that every global store instruction
+        // writes 256 contiguous bytes of the row: lane l stores the wave's own cells
+        // jbase + l + 64 i, read from the wave's staging row at rd[i] (-1: none).
+        float* rs;
+        int jbase;
+        int rd[C];
     };
 
     // All waves of the workgroup call run(); with H, wave W is the helper.
@@ -389,7 +401,8 @@ struct Forward {
                                                float* lds /* kBufs * kChunk * VS */,
                                                float* c0b /* H: 2 * kChunk column-0 values */,
                                                float* xh /* 2 * W * 64: chunk halo copies */, bool x4,
-                                               const ColMap& cm /* VS == kGatherVS: column map */) {
+                                               const ColMap& cm /* VS == kGatherVS: column map */,
+                                               float* rst = nullptr /* MODE 1: W * 64 * C row staging */) {
         const int wv = uniform((int)threadIdx.x >> 6);
         const int T = d.T, N = d.N;
         const int nch = (T + kChunk - 1) / kChunk;
@@ -436,6 +449,21 @@ struct Forward {
         const bool owner = uniform(own_w) == wv && l == own_l;
 
         State st;
+        if (MODE == 1) {
+            const int g0 = Geo::lane_of(wv, wv == 0 ? 0 : Geo::HL);  // first own useful lane
+            const int g1 = min(Geo::lane_of(wv, kWave - 1), L.G - 1);
+            const int jend = g1 >= g0 ? L.first(g1) + L.count(g1) - 1 : 0;
+            st.jbase = g0 < L.G ? L.first(g0) : N + 1;
+            const int nown = max(0, jend - st.jbase + 1);
+            st.rs = rst + wv * kWave * C;
+#pragma unroll
+            for (int i = 0; i < C; ++i) {
+                const int r = l + kWave * i;
+                int gg = 0, kk = 0;
+                if (r < nown) L.locate<C>(st.jbase + r - 1, gg, kk);
+                st.rd[i] = r < nown ? (gg - Geo::lane_of(wv, 0)) * C + kk : -1;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < C; ++k) st.cur[k] = -INFINITY;  // row 0, columns 1..N
 #pragma unroll
@@ -591,15 +619,15 @@ struct Forward {
             return;
         }
         int r = 0;
-        for (; r + kUnroll <= rows; r += kUnroll) {
+        for (; r + kU <= rows; r += kU) {
             const char* gb = bb + r * kRowBytes;
             const char* ga[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-            float hist[kUnroll];  // column N after each step (owner lane)
-            if (!WAVE0 || H || st.t + kUnroll < inf_from) {  // column 0 from LDS, or finite for the group
+            float hist[kU];  // column N after each step (owner lane)
+            if (!WAVE0 || H || st.t + kU < inf_from) {  // column 0 from LDS, or finite for the group
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
+                for (int u = 0; u < kU; ++u) {
                     step<!WAVE0 ? 0 : (H ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
                                                                  inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
@@ -607,16 +635,17 @@ struct Forward {
                 }
             } else {
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
+                for (int u = 0; u < kU; ++u) {
                     step<kColAny>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
                 }
             }
-            if (MODE == 0 && owner) {  // rows t-7 .. t at cn[t-8 .. t-1] (16-byte aligned)
-                float4* o = reinterpret_cast<float4*>(cn + st.t - kUnroll);
-                o[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
-                o[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+            if (MODE == 0 && owner) {  // rows t-kU+1 .. t at cn[t-kU .. t-1] (16-byte aligned)
+                float4* o = reinterpret_cast<float4*>(cn + st.t - kU);
+#pragma unroll
+                for (int i = 0; i < kU / 4; ++i)
+                    o[i] = make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]);
             }
         }
         for (; r < rows; ++r) {
@@ -719,11 +748,22 @@ struct Forward {
             float* row = tr + (int64_t)(st.t + 1) * ((int64_t)N + 1);
             if (COL && lane_id() == 0)
                 row[0] = COL == 3 ? (st.t + 1 < inf_from ? c0[1] : INFINITY) : st.col0;
+            float* rw = st.rs + lane_id() * C;  // every lane stages its C slots (in-order LDS)
+            if constexpr (C % 4 == 0) {
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
-                const int j = f + k;
-                if (!halo && k < cnt && j <= N) row[j] = st.cur[k];
+                for (int k = 0; k < C; k += 4)
+                    *reinterpret_cast<float4*>(rw + k) = make_float4(st.cur[k], st.cur[k + 1], st.cur[k + 2], st.cur[k + 3]);
+            } else if constexpr (C % 2 == 0) {
+#pragma unroll
+                for (int k = 0; k < C; k += 2) *reinterpret_cast<float2*>(rw + k) = make_float2(st.cur[k], st.cur[k + 1]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < C; ++k) rw[k] = st.cur[k];
             }
+            float* own = row + st.jbase + lane_id();
+#pragma unroll
+            for (int i = 0; i < C; ++i)
+                if (st.rd[i] >= 0) own[kWave * i] = st.rs[st.rd[i]];  // (nt stores: 25% slower)
         }
     }
 };
@@ -987,6 +1027,7 @@ struct AlignArgs {
 // Latency buckets (H) claim more than half of a CU's 160 KB LDS so that the dispatcher
 // places one workgroup per CU: two 8-wave workgroups on one CU would share its SIMDs
 // (4 waves per SIMD) while other CUs idle.
+
 constexpr int kLatencyLdsFloats = 84 * 1024 / 4;
 
 // Column-map LDS of the gather (large-vocabulary) instantiations.
@@ -1013,8 +1054,7 @@ __device__ __forceinline__ bool prepare_colmap(ColMapLds<VS>& m, ColMap& cm, con
 }
 
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H))
-    __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(AlignArgs a) {
+__device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 3 * kChunk * VS ? kLatencyLdsFloats : 3 * kChunk * VS)
                                  : 2 * kChunk * VS;
     __shared__ float lds[kLdsFloats];
@@ -1081,6 +1121,17 @@ __global__ __launch_bounds__(kWave*(W + H))
     WX_STAMP_RT(5);
 }
 
+template <int C, int VS, int W, int H>
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
+    AlignArgs a) {
+    align_dp_body<C, VS, W, H>(a);
+}
+
+template <int C, int VS, int W, int H>
+void launch_align_dp(dim3 grid, hipStream_t s, const AlignArgs& a) {
+    hipLaunchKernelGGL((align_dp_kernel<C, VS, W, H>), grid, dim3(kWave * (W + H)), 0, s, a);
+}
+
 struct TrellisArgs {
     const float* em;
     const int64_t* em_off;
@@ -1098,6 +1149,7 @@ __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
     __shared__ float lds[2 * kChunk * VS];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ ColMapLds<VS> cml;
+    __shared__ __attribute__((aligned(16))) float rst[W * kWave * C];
     const int seg = blockIdx.x;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     if (bucket_id(d.N) != bucket_make(C, W, 0)) return;
@@ -1115,7 +1167,7 @@ __global__ __launch_bounds__(kWave * W) void trellis_kernel(TrellisArgs a) {
     }
     const float* E = a.em + d.row0 * a.V;
     Forward<C, VS, 1, W, false>::run(d, E, a.V, a.tok, nullptr, nullptr, nullptr, tr, lds, nullptr, xh, a.x4 != 0,
-                                     cm);
+                                     cm, rst);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1684,10 +1736,9 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
     return fork_join(st, n, [&](int i, hipStream_t s) {
 #define WX_LAUNCH_ALIGN(CC, WW, HH)                                                                  \
         if (ids[i] == bucket_make(CC, WW, HH)) {                                                       \
-            const dim3 block(kWave * (WW + HH));                                                       \
-            if (V <= 32) hipLaunchKernelGGL((align_dp_kernel<CC, 32, WW, HH>), grid, block, 0, s, a);   \
-            else if (V <= 64) hipLaunchKernelGGL((align_dp_kernel<CC, 64, WW, HH>), grid, block, 0, s, a); \
-            else hipLaunchKernelGGL((align_dp_kernel<CC, kGatherVS, WW, HH>), grid, block, 0, s, a);    \
+            if (V <= 32) launch_align_dp<CC, 32, WW, HH>(grid, s, a);                                  \
+            else if (V <= 64) launch_align_dp<CC, 64, WW, HH>(grid, s, a);                             \
+            else launch_align_dp<CC, kGatherVS, WW, HH>(grid, s, a);                                   \
         }
         WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
