@@ -93,7 +93,8 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
  * merge_repeats segment; a successful path always yields exactly N_s of them).
  * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None),
  * 2 not computed: V > 64 and the segment uses more than WX_MAX_SEGMENT_COLUMNS distinct
- * emission columns.
+ * emission columns, 3 not computed: a split segment's cross-CU hand-off timed out (only
+ * if another kernel starves the segment's CUs for ~0.1 s; re-run the call).
  * min_N/max_N/sum_T describe the batch (host values). */
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
@@ -107,10 +108,20 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
  *   WX_MODE_AUTO        latency shape for batches of <= 256 segments, else throughput;
  *   WX_MODE_THROUGHPUT  one wave per segment up to 2048 tokens (most segments in flight);
  *   WX_MODE_LATENCY     each segment's columns spread over up to 8 waves (shortest time
- *                       per segment when the batch cannot fill the GPU).
+ *                       per segment when the batch cannot fill the GPU); when the device
+ *                       has >= 2 CUs per segment, over up to 4 CUs (split parts).
  * wx_align_dp == wx_align_dp_mode(..., WX_MODE_AUTO) unless the environment variable
- * WX_ALIGN_MODE=0/1 forces a shape (benchmarking). */
-enum { WX_MODE_AUTO = -1, WX_MODE_THROUGHPUT = 0, WX_MODE_LATENCY = 1 };
+ * WX_ALIGN_MODE=0/1 forces a shape (benchmarking); WX_PARTS=1..4 forces the parts per
+ * segment of latency launches. */
+enum {
+    WX_MODE_AUTO = -1,
+    WX_MODE_THROUGHPUT = 0,
+    WX_MODE_LATENCY = 1,     /* parts per segment chosen from the device's CU count */
+    WX_MODE_LATENCY_1CU = 2, /* latency shape, one CU per segment */
+    WX_MODE_SPLIT2 = 12,     /* latency shape, 2 / 3 / 4 CUs per segment */
+    WX_MODE_SPLIT3 = 13,
+    WX_MODE_SPLIT4 = 14
+};
 int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V,
                      const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
                      int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T,

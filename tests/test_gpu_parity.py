@@ -19,6 +19,8 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
+# throughput; latency (auto parts); latency on one CU; split over 2 / 3 / 4 CUs
+MODES = [0, 1, 2, 12, 13, 14]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -107,7 +109,7 @@ def _check_vs_oracle(cases, tag, mode=-1):
     return mism
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("V", [29, 32, 40, 64])
 def test_align_dp_random_mixed_buckets_vs_oracle(V, mode):
     rng = np.random.default_rng(V)
@@ -128,10 +130,16 @@ def _capacity(C, W):
 
 
 THROUGHPUT_BUCKETS = [(1, 1), (2, 1), (4, 1), (6, 1), (8, 1), (8, 2), (8, 4), (8, 8), (16, 8)]
+SPLIT_BUCKETS = [(1, 3), (1, 4), (2, 3), (4, 3)]
+
+
+def _split_capacity(C, W, P):
+    """Tokens a split bucket holds: the chunk halo runs through all W * P virtual waves."""
+    return C * (64 + (W * P - 1) * (64 - (32 + C - 1) // C))
 LATENCY_BUCKETS = [(1, 1), (1, 3), (1, 7), (2, 7), (4, 7), (8, 7), (16, 8)]
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", MODES)
 def test_align_dp_bucket_capacity_edges(mode):
     """N at every bucket capacity and one past it (column N in the last lane of the last wave,
     halo lanes holding column N's left neighbours), in both launch shapes, V=32 (16-byte
@@ -142,12 +150,20 @@ def test_align_dp_bucket_capacity_edges(mode):
         cap = _capacity(C, W)
         if cap <= 4001 or (mode == 0 and cap <= 8000):
             Ns.update({cap, cap + 1})
+    if mode != 0:  # split buckets (every part count: the auto mode picks one from the batch size)
+        for P in (2, 3, 4):
+            for C, W in SPLIT_BUCKETS:
+                cap = _split_capacity(C, W, P)
+                Ns.update({cap, cap + 1})
     for V in (32, 29):
         cases = []
         for N in sorted(Ns):
             T = N + int(rng.integers(2, 70))
             cases += _random_cases(rng, 1, (T, T + 1), (N, N + 1), V, blank=0)
         _check_vs_oracle(cases, f"edges V{V} mode {mode}", mode)
+        if mode != 0:  # a split launch runs the bucket of its longest segment: one batch per N too
+            for c in cases:
+                _check_vs_oracle([c, cases[0]], f"edge N={len(c['tokens'])} V{V} mode {mode}", mode)
 
 
 def _large_vocab_cases(rng, V, n, T_range, N_range, distinct):
@@ -169,7 +185,7 @@ def _large_vocab_cases(rng, V, n, T_range, N_range, distinct):
     return cases
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("V", [100, 1000, 4000])
 def test_align_dp_large_vocabulary_vs_oracle(V, mode):
     """V > 64 (e.g. the ja/zh wav2vec2 character vocabularies): each segment's used columns
@@ -242,7 +258,7 @@ def test_trellis_every_bucket_vs_oracle(V):
         assert np.array_equal(got, exp, equal_nan=True), f"V{V} segment {s_} (T={T}, N={N})"
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", MODES)
 def test_align_dp_long_segments_and_chunk_edges(mode):
     """T > 8192 (walk change masks in global memory instead of LDS), T at multiples of the
     32-row chunk and one off, T < 32, N = 1 and N = T - 1."""
@@ -261,7 +277,7 @@ def test_align_dp_config2_batch_vs_oracle():
     """BASELINE config 2: 64 x 30 s segments (T=1499, V=32, N~U[300,500])."""
     rng = np.random.default_rng(2)
     cases = _random_cases(rng, 64, (1499, 1500), (300, 501), 32, blank=0)
-    for mode in (0, 1):
+    for mode in MODES:
         _check_vs_oracle(cases, f"cfg2 mode {mode}", mode)
 
 
@@ -269,7 +285,7 @@ def test_align_dp_config5_long_form_vs_oracle():
     """BASELINE config 5: DE large-xlsr-shaped, T=2999, V=40, N~900."""
     rng = np.random.default_rng(5)
     cases = _random_cases(rng, 8, (2999, 3000), (850, 951), 40, blank=0)
-    for mode in (0, 1):
+    for mode in MODES:
         _check_vs_oracle(cases, f"cfg5 mode {mode}", mode)
 
 

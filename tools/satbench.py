@@ -112,15 +112,28 @@ def child(args):
         if args.phases:
             import ctypes
             lib = _lib.load()
-            n = min(S, 8192)
+            n = min(S * args.parts, 8192)  # one row per workgroup (split: S * parts)
             buf = (ctypes.c_ulonglong * (6 * n))()
             lib.wx_debug_phases(buf, n)
             ph = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)
             fwd, walk, mrg = ph[:, 1] - ph[:, 0], ph[:, 2] - ph[:, 1], ph[:, 3] - ph[:, 2]
+            if args.parts > 1:
+                pf = fwd.reshape(-1, args.parts)
+                out[case]["fwd_by_part_med"] = [float(np.median(pf[:, i])) for i in range(args.parts)]
+                ent = (ph[:, 4] - ph[:, 4].min()).reshape(-1, args.parts) / 100.0
+                out[case]["entry_by_part_med_us"] = [float(np.median(ent[:, i])) for i in range(args.parts)]
+                ex = (ph[:, 5] - ph[:, 4].min()).reshape(-1, args.parts) / 100.0
+                out[case]["exit_by_part_med_us"] = [float(np.median(ex[:, i])) for i in range(args.parts)]
+                out[case]["exit_max_us"] = float(ex.max())
             out[case]["phases_cyc_med"] = {"forward": float(np.median(fwd)), "walk": float(np.median(walk)),
                                            "merge": float(np.median(mrg)), "per_step_fwd": float(np.median(fwd)) / T,
                                            "per_step_walk": float(np.median(walk)) / T,
                                            "walk_max": float(walk.max()), "fwd_max": float(fwd.max())}
+            lbuf = (ctypes.c_ulonglong * (n * 16 * 3))()
+            lib.wx_debug_loop(lbuf, n)
+            lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)
+            out[case]["loop_med_per_wave"] = [[float(np.median(lp[:, w, i])) for i in range(3)] for w in range(8)
+                                              if lp[:, w, 0].max() > 0]
             rt = (ph[:, 5] - ph[:, 4]) / 100.0  # s_memrealtime ticks at 100 MHz -> us
             out[case]["seg_us_med"] = float(np.median(rt))
             ent = (ph[:, 4] - ph[:, 4].min()) / 100.0
@@ -139,6 +152,7 @@ def main():
     ap.add_argument("--mode", type=int, default=-1)
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--phases", action="store_true", help="library built with -DWX_PHASE_TIMING")
+    ap.add_argument("--parts", type=int, default=1, help="workgroups per segment of the timed launch (phases)")
     args = ap.parse_args()
     if args.child:
         child(args)
@@ -148,7 +162,7 @@ def main():
         env = dict(os.environ, WX_LIB_PATH=os.path.abspath(lib), PYTHONHASHSEED="0")
         t0 = time.time()
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--cases", args.cases,
-                            "--steps", str(args.steps), "--mode", str(args.mode)] + (["--phases"] if args.phases else []),
+                            "--steps", str(args.steps), "--mode", str(args.mode)] + (["--phases", "--parts", str(args.parts)] if args.phases else []),
                            env=env, capture_output=True, text=True, timeout=600)
         line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
         if r.returncode != 0 or not line:
@@ -160,6 +174,10 @@ def main():
             print(f"  {case:9s} {v['ms_med']:9.4f} ms  {v['cells_per_s']:.3e} cells/s  frac {v['frac']:.3f}", flush=True)
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
+                for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
+                          "loop_med_per_wave"):
+                    if k in v:
+                        print(f"            {k} {v[k]}", flush=True)
     libs = list(results)
     for lib in libs[1:]:
         for case in results[lib]:

@@ -186,7 +186,8 @@ def _validate(b: Batch):
         raise WXError(f"a segment has {b.max_N} tokens; the kernel supports up to {MAX_TOKENS}")
 
 
-MODE_AUTO, MODE_THROUGHPUT, MODE_LATENCY = -1, 0, 1
+MODE_AUTO, MODE_THROUGHPUT, MODE_LATENCY, MODE_LATENCY_1CU = -1, 0, 1, 2
+MODE_SPLIT2, MODE_SPLIT3, MODE_SPLIT4 = 12, 13, 14  # latency shape over 2 / 3 / 4 CUs per segment
 
 
 def align_dp(b: Batch, mode: int = MODE_AUTO):

@@ -36,6 +36,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <mutex>
 
 #include "../../include/wx_align.h"
@@ -314,9 +316,9 @@ __device__ unsigned long long wx_phase[8192 * 6];
 __device__ unsigned long long wx_loop[8192 * 16 * 3];
 #define WX_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define WX_STAMP(i) \
-    if (threadIdx.x == 0 && seg < 8192) wx_phase[seg * 6 + (i)] = __builtin_amdgcn_s_memtime()
+    if (threadIdx.x == 0 && blockIdx.x < 8192) wx_phase[blockIdx.x * 6 + (i)] = __builtin_amdgcn_s_memtime()
 #define WX_STAMP_RT(i) \
-    if (threadIdx.x == 0 && seg < 8192) wx_phase[seg * 6 + (i)] = __builtin_amdgcn_s_memrealtime()
+    if (threadIdx.x == 0 && blockIdx.x < 8192) wx_phase[blockIdx.x * 6 + (i)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define WX_STAMP(i)
 #define WX_STAMP_RT(i)
@@ -340,6 +342,40 @@ __device__ unsigned long long wx_loop[8192 * 16 * 3];
 // H (helper): one more wave per workgroup stages the emission rows two chunks ahead and
 // computes column 0 (the fp64 cumsum, +inf rows) and q0 = exp(em[t,0]) one chunk ahead, so
 // the column-1 wave reads column 0 from LDS instead of running the fp64 chain per step.
+// Split segments (latency mode, few segments): one segment's columns are spread over P
+// workgroups ("parts", one per CU), continuing the chunk halo across CUs.  Virtual wave
+// vw = part * W + wv; the first HL lanes of a part's wave 0 mirror the last HL lanes of
+// the previous part's wave W-1, handed over once per 32-row chunk through global memory
+// as 8-byte {value, tag} granules (one sc1 store each; the tag carries the launch epoch and
+// the chunk, so a granule is valid on its own — no flag, no fence).  A part lags its
+// predecessor by about one chunk plus the hand-off latency; the consumer prefetches the
+// next chunk's granules one chunk ahead.  Each part then arrives at a per-segment counter;
+// the last to arrive runs the argmax, the walk and merge_repeats.
+constexpr int kMaxParts = 4;
+constexpr int kHaloCells = 40;  // >= HL * C = ceil(32 / C) * C for every C
+constexpr int kMaxSpin = 1 << 16;
+#ifndef WX_XSLACK
+#define WX_XSLACK 2
+#endif
+constexpr int kXSlack = WX_XSLACK;  // chunks a part trails its predecessor by (>= 1)  // granule re-reads (~1 us each) before a hand-off counts as lost
+
+struct Split {
+    int p, P;         // this part, parts per segment
+    int lanes;        // bitmap word stride: 64 * W * P
+    unsigned tag;     // epoch << 12 (the chunk index goes in the low 12 bits)
+    uint64_t* xin;    // granules from part p-1: [chunk][kHaloCells] (p > 0)
+    uint64_t* xout;   // granules to part p+1 (p < P-1)
+    int xstride;      // granules per chunk block of one segment boundary
+};
+
+__device__ __forceinline__ void granule_store(uint64_t* g, float v, unsigned tag) {
+    const uint64_t x = ((uint64_t)tag << 32) | (uint64_t)__builtin_bit_cast(unsigned, v);
+    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dwordx2 sc1
+}
+__device__ __forceinline__ uint64_t granule_load(const uint64_t* g) {
+    return __hip_atomic_load(const_cast<uint64_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int C, int W>
 struct Geometry {
     static constexpr int HL = W > 1 ? (32 + C - 1) / C : 0;  // halo lanes per wave >= 1
@@ -361,16 +397,16 @@ struct Geometry {
     }
 };
 
-template <int C, int VS, int MODE, int W, bool H>
+template <int C, int VS, int MODE, int W, bool H, bool SP = false>
 struct Forward {
     static constexpr int kRowBytes = VS * 4;
-    static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves)
-    static constexpr int kBufs = H ? 3 : 2;   // emission chunk buffers in LDS
+    static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves; SP: Split::lanes)
+    static constexpr int kBufs = H ? 4 : 2;   // emission chunk buffers in LDS
     // Software-pipelined LDS operands where the extra registers keep the occupancy that
     // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
     static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
-    using Geo = Geometry<C, W>;
+    using Geo = Geometry<C, (SP ? 2 : W)>;  // SP: always a halo (the waves span P parts)
     // Steps per unrolled group of the non-pipelined chunk (hipcc hoists the group's LDS
     // loads; a multiple of 4: column-N history is stored as float4).
     static constexpr int kU = C >= 8 ? WX_C8_UNROLL : kUnroll;
@@ -391,8 +427,32 @@ struct Forward {
         int rd[C];
     };
 
+    // SP: make xpre[] hold chunk q's halo granules (lanes < HL, C each), re-reading until
+    // every tag matches.  Returns whether they were already there; bounded (sets lost).
+    __device__ __forceinline__ static bool xwait(const uint64_t* xin, int xstride, int q, int l, unsigned tag,
+                                                 uint64_t (&xpre)[C], bool& lost) {
+        constexpr int HL = Geometry<C, 2>::HL;
+        const unsigned want = tag | (unsigned)(q & 0xFFF);
+        const uint64_t* gi = xin + (int64_t)q * xstride + l * C;
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < C; ++k) ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
+        const bool first = __all(ok);
+        for (int it = 0; !lost && !__all(ok) && it < kMaxSpin; ++it) {
+            __builtin_amdgcn_s_sleep(2);
+            ok = true;
+#pragma unroll
+            for (int k = 0; k < C; ++k) {
+                if (l < HL) xpre[k] = granule_load(gi + k);
+                ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
+            }
+        }
+        lost = lost || !__all(ok);
+        return first;
+    }
+
     // All waves of the workgroup call run(); with H, wave W is the helper.
-    __device__ __forceinline__ static void run(const SegDesc& d, const float* __restrict__ E, int V,
+    __device__ __forceinline__ static bool run(const SegDesc& d, const float* __restrict__ E, int V,
                                                const int32_t* __restrict__ tok,
                                                unsigned* __restrict__ bits,  // MODE 0: segment's bitmap
                                                float* __restrict__ q0,        // MODE 0: exp(em[t,0]) per row
@@ -402,21 +462,24 @@ struct Forward {
                                                float* c0b /* H: 2 * kChunk column-0 values */,
                                                float* xh /* 2 * W * 64: chunk halo copies */, bool x4,
                                                const ColMap& cm /* VS == kGatherVS: column map */,
-                                               float* rst = nullptr /* MODE 1: W * 64 * C row staging */) {
+                                               float* rst = nullptr /* MODE 1: W * 64 * C row staging */,
+                                               const Split* sp = nullptr /* SP */) {
         const int wv = uniform((int)threadIdx.x >> 6);
+        const int vw = SP ? sp->p * W + wv : wv;  // virtual wave (SP: across parts)
+        const int lanes = SP ? sp->lanes : kLanes;
         const int T = d.T, N = d.N;
         const int nch = (T + kChunk - 1) / kChunk;
         if (H && wv == W) {
-            helper(d, E, V, lds, c0b, nch, x4, cm);
-            return;
+            helper(d, E, V, lds, c0b, nch, x4, cm, !SP || sp->p == 0);
+            return false;
         }
         const int l = lane_id();
-        const Layout L = Layout::make(C, N, kLanes);
+        const Layout L = Layout::make(C, N, lanes);
         if (MODE == 1) {
             if (threadIdx.x == 0) tr[0] = col0_value(0, 0.0, T, N);
             for (int j = (int)threadIdx.x + 1; j <= N; j += kLanes) tr[j] = -INFINITY;
         }
-        if (W > 1 && wv > 0 && Geo::lane_of(wv, Geo::HL) >= L.G) {
+        if ((W > 1 || SP) && vw > 0 && Geo::lane_of(vw, Geo::HL) >= L.G) {
             // no column of this wave exists: keep the barrier count (and, without a helper,
             // this wave's share of the staging)
             if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
@@ -427,10 +490,14 @@ struct Forward {
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
                                       lds + ((q + 1) % kBufs) * kChunk * VS, x4, cm);
             }
-            return;
+            return false;
         }
-        const int g = Geo::lane_of(wv, l);  // useful lane this lane computes
-        const bool halo = wv > 0 && l < Geo::HL;
+        const int g = Geo::lane_of(vw, l);  // useful lane this lane computes
+        const bool halo = vw > 0 && l < Geo::HL;
+        // SP: wave W-1 hands its last HL lanes to the next part (if that part has columns);
+        // wave 0 of parts > 0 takes its halo lanes from the previous part.
+        const bool xpub = SP && wv == W - 1 && sp->p + 1 < sp->P && Geo::lane_of(vw + 1, Geo::HL) < L.G;
+        const bool xsub = SP && wv == 0 && sp->p > 0;
         const int f = L.first(g), cnt = L.count(g);
         const bool is_short = g < L.n_short;
         // per-slot LDS byte offsets of em[., tok[j-1]]
@@ -446,12 +513,12 @@ struct Forward {
         // column N = slot C-1 of useful lane G-1
         int own_w, own_l;
         Geo::owner(L.G - 1, own_w, own_l);
-        const bool owner = uniform(own_w) == wv && l == own_l;
+        const bool owner = uniform(own_w) == vw && l == own_l;
 
         State st;
         if (MODE == 1) {
-            const int g0 = Geo::lane_of(wv, wv == 0 ? 0 : Geo::HL);  // first own useful lane
-            const int g1 = min(Geo::lane_of(wv, kWave - 1), L.G - 1);
+            const int g0 = Geo::lane_of(vw, vw == 0 ? 0 : Geo::HL);  // first own useful lane
+            const int g1 = min(Geo::lane_of(vw, kWave - 1), L.G - 1);
             const int jend = g1 >= g0 ? L.first(g1) + L.count(g1) - 1 : 0;
             st.jbase = g0 < L.G ? L.first(g0) : N + 1;
             const int nown = max(0, jend - st.jbase + 1);
@@ -461,7 +528,7 @@ struct Forward {
                 const int r = l + kWave * i;
                 int gg = 0, kk = 0;
                 if (r < nown) L.locate<C>(st.jbase + r - 1, gg, kk);
-                st.rd[i] = r < nown ? (gg - Geo::lane_of(wv, 0)) * C + kk : -1;
+                st.rd[i] = r < nown ? (gg - Geo::lane_of(vw, 0)) * C + kk : -1;
             }
         }
 #pragma unroll
@@ -474,6 +541,14 @@ struct Forward {
         const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
 
         if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
+        uint64_t xpre[C];           // SP: granules of the next chunk's halo (prefetched)
+        bool xlost = false;         // SP: a hand-off timed out
+#pragma unroll
+        for (int k = 0; k < C; ++k) xpre[k] = 0;
+        if (SP && xsub && nch > 1 && l < Geo::HL) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) xpre[k] = granule_load(sp->xin + sp->xstride + l * C + k);
+        }
 #ifdef WX_PHASE_TIMING
         unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0;
 #endif
@@ -486,13 +561,42 @@ struct Forward {
 #pragma unroll
                 for (int k = 0; k < C; ++k) xq[wv * kWave + (l - (kWave - Geo::HL)) * C + k] = st.cur[k];
             }
+            if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
+                uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
+#pragma unroll
+                for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag | (unsigned)(q & 0xFFF));
+            }
             WX_T(c1);
-            wait_vm();
+            if (!H) wait_vm();  // this wave's staging (with a helper, DP waves stage nothing)
             __syncthreads();
             WX_T(c2);
-            if (W > 1 && q > 0 && halo) {
+            if (W > 1 && q > 0 && halo && wv > 0) {
 #pragma unroll
                 for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
+            }
+            if (SP && xsub && q > 0) {
+                // Halo of row 32q from the previous part: the granules prefetched one chunk
+                // ago.  A part must trail its predecessor by more than a chunk plus the
+                // hand-off latency for the prefetch to find them; at chunk 1, and after any
+                // miss, it therefore also waits for the next chunk's granules (re-building
+                // that slack once instead of paying a round trip every chunk).  Waits are
+                // bounded: a lost hand-off marks the segment failed instead of hanging.
+                const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost);
+                if (l < Geo::HL) {
+#pragma unroll
+                    for (int k = 0; k < C; ++k) st.cur[k] = __builtin_bit_cast(float, (unsigned)xpre[k]);
+                }
+                if ((missed || q == 1) && q + kXSlack < nch) {  // (re)build the slack
+                    uint64_t tmp[C];
+#pragma unroll
+                    for (int k = 0; k < C; ++k) tmp[k] = 0;
+                    xwait(sp->xin, sp->xstride, q + kXSlack, l, sp->tag, tmp, xlost);
+                }
+                if (q + 1 < nch && l < Geo::HL) {
+                    const uint64_t* gn = sp->xin + (int64_t)(q + 1) * sp->xstride + l * C;
+#pragma unroll
+                    for (int k = 0; k < C; ++k) xpre[k] = granule_load(gn + k);
+                }
             }
             if (!H) {
                 if (q + 1 < nch)
@@ -503,7 +607,7 @@ struct Forward {
             const char* bb = reinterpret_cast<const char*>(buf);
             const float* c0q = H ? c0b + (q & 1) * kChunk : nullptr;
             WX_T(c3);
-            if (wv == 0)
+            if (vw == 0)
                 chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else
                 chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
@@ -517,7 +621,7 @@ struct Forward {
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
-                    if (!halo) bits[((int64_t)q * C + k) * kLanes + g] = (sh == 0) ? st.w[k] : (st.w[k] << sh);
+                    if (!halo) bits[((int64_t)q * C + k) * lanes + g] = (sh == 0) ? st.w[k] : (st.w[k] << sh);
                     st.w[k] = 0u;
                 }
             }
@@ -530,34 +634,47 @@ struct Forward {
             o[2] = acc_other;
         }
 #endif
+        return xlost;
     }
 
     // The helper wave (H): mirrors the DP waves' barriers.  Before barrier q, chunks q and
     // q+1 are staged and column 0 of chunk q is in c0b[q & 1].  (q0 is filled after the
     // forward pass, while wave 0 walks: fill_q0.)
     __device__ static void helper(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* c0b,
-                                  int nch, bool x4, const ColMap& cm) {
+                                  int nch, bool x4, const ColMap& cm, bool col0) {
         const int T = d.T, N = d.N;
         const int inf_from = T + 1 - N;
         double acc = 0.0;  // sum of em[0..t-1, 0], uniform
-        if (nch > 0) stage_rows<VS, 1, true>(E, V, 0, min(kChunk, T), lds, x4, cm);
-        if (nch > 1) stage_rows<VS, 1, true>(E, V, kChunk, min(kChunk, T - kChunk), lds + kChunk * VS, x4, cm);
+        // Rows are staged three chunks ahead (four LDS buffers) and waited for one chunk
+        // ahead, so each chunk's loads have two chunk times to land: at chunk q only the
+        // loads of chunk q+2 may still be in flight (vmcnt = that chunk's instruction
+        // count: 4 for 16-byte staging, 32 for row staging; gathers drain fully).
+        for (int i = 0; i < 3 && i < nch; ++i)
+            stage_rows<VS, 1, true>(E, V, i * kChunk, min(kChunk, T - i * kChunk), lds + i * kChunk * VS, x4, cm);
         wait_vm();
-        column0(0, T, inf_from, lds, c0b, acc);
+        if (col0) column0(0, T, inf_from, lds, c0b, acc);
 #ifdef WX_PHASE_TIMING
         unsigned long long acc_c0 = 0, acc_bar = 0, acc_other = 0;
 #endif
         for (int q = 0; q < nch; ++q) {
             WX_T(h0);
-            wait_vm();
+            // chunk q+1 must have landed; chunk q+2 (staged at q-1) may still be in flight
+            if (q + 2 < nch && T - (q + 2) * kChunk >= kChunk && VS != kGatherVS) {
+                if (x4 && VS == 32)
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            } else {
+                wait_vm();
+            }
             WX_T(h1);
             __syncthreads();
             WX_T(h2);
-            if (q + 2 < nch)
-                stage_rows<VS, 1, true>(E, V, (q + 2) * kChunk, min(kChunk, T - (q + 2) * kChunk),
-                                        lds + ((q + 2) % kBufs) * kChunk * VS, x4, cm);
+            if (q + 3 < nch)
+                stage_rows<VS, 1, true>(E, V, (q + 3) * kChunk, min(kChunk, T - (q + 3) * kChunk),
+                                        lds + ((q + 3) % kBufs) * kChunk * VS, x4, cm);
             WX_T(h3);
-            if (q + 1 < nch) column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
+            if (col0 && q + 1 < nch) column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
             WX_T(h4);
 #ifdef WX_PHASE_TIMING
             acc_c0 += h4 - h3;
@@ -1001,6 +1118,39 @@ __host__ __device__ __forceinline__ int bucket_id(int N, int mode = 0) {
 // bitmap words per 32-step block of a segment in bucket `id`
 __host__ __device__ __forceinline__ int bucket_cells_total(int id) { return bucket_C(id) * kWave * bucket_W(id); }
 
+// Split buckets (C cells per lane, W DP waves + 1 helper per part, P parts): the chunk
+// halo runs through all W * P virtual waves.  Segments too long for the widest split bucket
+// use the single-CU latency buckets in the same launch.
+#define WX_SPLIT_BUCKETS(X) X(1, 3) X(1, 4) X(2, 3) X(4, 3)
+constexpr int kSplitFlag = 1 << 20;
+__host__ __device__ constexpr int split_capacity(int C, int W, int P) {
+    return C * (kWave + (W * P - 1) * (kWave - (32 + C - 1) / C));
+}
+#define WX_PICK_SPLIT(CC, WW) \
+    if (N <= split_capacity(CC, WW, P)) return bucket_make(CC, WW, 1) | kSplitFlag;
+__host__ __device__ __forceinline__ int split_bucket_id(int N, int P) {
+    WX_SPLIT_BUCKETS(WX_PICK_SPLIT)
+    return bucket_id(N, 1);
+}
+#undef WX_PICK_SPLIT
+
+// A split launch runs ONE split kernel (the bucket of the batch's longest segment): its
+// grid is S * P workgroups, one per CU, and a second split grid would queue behind it
+// (measured: workgroups of the second kernel started up to 70 us late).  Shorter segments
+// leave that bucket's extra waves idle.  Segments beyond its capacity use the single-CU
+// latency buckets.
+__host__ __device__ __forceinline__ int split_capacity_of(int id, int P) {
+    return split_capacity(bucket_C(id & ~kSplitFlag), bucket_W(id & ~kSplitFlag), P);
+}
+// Layout::make needs N >= ceil(N/C) * (C-1) (at most one missing cell per lane); the
+// per-N buckets always satisfy it, a launch-wide split bucket may not for short segments,
+// which then take a throughput bucket (one wave, small LDS: it shares CUs with the parts).
+__host__ __device__ constexpr bool layout_fits(int N, int C) { return N >= (N + C - 1) / C * (C - 1); }
+__host__ __device__ __forceinline__ int launch_split_bucket(int N, int P, int split_id) {
+    if (N > split_capacity_of(split_id, P)) return bucket_id(N, 1);
+    return layout_fits(N, bucket_C(split_id & ~kSplitFlag)) ? split_id : bucket_id(N, 0);
+}
+
 struct AlignArgs {
     const float* em;
     const int64_t* em_off;
@@ -1021,7 +1171,27 @@ struct AlignArgs {
     float* q0;       // workspace: sum_T floats
     unsigned* cmask; // workspace: walk change masks, (floor(row0/32) + seg) words per segment
     float* cn;       // workspace: column N history, segment at (row0 + 4 seg) & ~3
+    int parts;       // split launches: workgroups (CUs) per segment, else 1
+    int split_id;    // split launches: the one split bucket (segments up to its capacity)
+    unsigned epoch;  // split launches: per-launch tag of the hand-off granules and counters
+    uint64_t* xg;    // workspace: hand-off granules, (floor(row0/32) + seg + q) * 3 * 40
+    unsigned* arrive;// workspace: per-segment arrival counters (epoch << 8 | count)
 };
+
+// Per-segment arrival of a split segment's parts; true for the last to arrive.  The word
+// is epoch << 8 | count (bit 7: a part lost a hand-off), so stale or uninitialised
+// workspace never needs clearing.  Returns the word after this arrival.
+__device__ unsigned split_arrive(unsigned* c, unsigned epoch, bool lost) {
+    const unsigned ep = epoch & 0xFFFFFFu;
+    unsigned old = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        const unsigned cur = ((old >> 8) == ep) ? (old & 0xFFu) : 0u;
+        const unsigned nw = (ep << 8) | ((cur & 0x7Fu) + 1u) | (cur & 0x80u) | (lost ? 0x80u : 0u);
+        if (__hip_atomic_compare_exchange_strong(c, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return nw;
+    }
+}
 
 
 // Latency buckets (H) claim more than half of a CU's 160 KB LDS so that the dispatcher
@@ -1053,22 +1223,25 @@ __device__ __forceinline__ bool prepare_colmap(ColMapLds<VS>& m, ColMap& cm, con
     return cm.n <= kGatherVS;
 }
 
-template <int C, int VS, int W, int H>
+template <int C, int VS, int W, int H, bool SP = false>
 __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
-    constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 3 * kChunk * VS ? kLatencyLdsFloats : 3 * kChunk * VS)
+    constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 4 * kChunk * VS ? kLatencyLdsFloats : 4 * kChunk * VS)
                                  : 2 * kChunk * VS;
     __shared__ float lds[kLdsFloats];
     __shared__ float c0b[H ? 2 * kChunk : 1];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
-    __shared__ int tsb[2];
+    __shared__ int tsb[3];
     __shared__ ColMapLds<VS> cml;
-    const int seg = blockIdx.x;
+    const int P = SP ? a.parts : 1;
+    const int seg = SP ? (int)blockIdx.x / P : (int)blockIdx.x;
+    const int part = SP ? (int)blockIdx.x - seg * P : 0;
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
-    if (bucket_id(d.N, a.mode) != bucket_make(C, W, H)) return;  // another instantiation owns it
+    const int want = (SP || a.parts > 1) ? launch_split_bucket(d.N, a.parts, a.split_id) : bucket_id(d.N, a.mode);
+    if (want != (bucket_make(C, W, H) | (SP ? kSplitFlag : 0))) return;  // another instantiation owns it
     const int lane = (int)threadIdx.x;
     if (d.N <= 0 || d.T <= 0) {
-        if (lane == 0) {
+        if (lane == 0 && part == 0) {
             a.t_start[seg] = 0;
             a.status[seg] = 1;
         }
@@ -1076,7 +1249,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     }
     ColMap cm;
     if (!prepare_colmap(cml, cm, a.tok + d.tok0, d.N, d.blank, a.V)) {
-        if (lane == 0) {
+        if (lane == 0 && part == 0) {
             a.t_start[seg] = 0;
             a.status[seg] = 2;  // more than kGatherVS distinct columns in one segment
         }
@@ -1088,10 +1261,46 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     float* cn = a.cn + ((d.row0 + 4 * (int64_t)seg) & ~(int64_t)3);
     WX_STAMP_RT(4);
     WX_STAMP(0);
-    Forward<C, VS, 0, W, H != 0>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm);
+    Split sp;
+    if (SP) {
+        sp.p = part;
+        sp.P = P;
+        sp.lanes = kWave * W * P;
+        sp.tag = a.epoch << 12;
+        sp.xstride = (kMaxParts - 1) * kHaloCells;
+        uint64_t* xs = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
+        sp.xin = xs + (part > 0 ? part - 1 : 0) * kHaloCells;
+        sp.xout = xs + part * kHaloCells;
+    }
+    if (SP && lane == 0) tsb[2] = 0;
+    const bool lost = Forward<C, VS, 0, W, H != 0, SP>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
+                                                            a.x4 != 0, cm, nullptr, &sp);
     WX_STAMP(1);
+    if (SP && lost) tsb[2] = 1;  // (any lane of wave 0)
     wait_vm();
     block_fence();
+    bool failed = false;
+    if (SP) {  // release this part's bits / column-N history; the last part to arrive goes on
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            wait_vm();
+            const unsigned w = split_arrive(a.arrive + seg, a.epoch, tsb[2] != 0);
+            tsb[0] = ((w & 0x7Fu) == (unsigned)P) ? 1 + (int)((w >> 7) & 1u) : 0;
+            if (tsb[0]) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                wait_vm();
+            }
+        }
+        __syncthreads();
+        if (tsb[0] == 0) {
+            WX_STAMP(2);
+            WX_STAMP(3);
+            WX_STAMP_RT(5);
+            return;
+        }
+        failed = tsb[0] == 2;
+        __syncthreads();
+    }
     int32_t* start = a.seg_start + d.tok0;
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
         const int ts = column_argmax(cn, d.T);
@@ -1100,7 +1309,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
             tsb[0] = ts;
         }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W), d.N, ts, cmask);
+        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W * P), d.N, ts, cmask);
         if (b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
@@ -1114,8 +1323,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     const int ts = tsb[0];
     const bool ok = tsb[1] != 0;
     WX_STAMP(2);
-    if (lane == 0) a.status[seg] = ok ? 0 : 1;
-    if (!ok) return;
+    if (lane == 0) a.status[seg] = failed ? 3 : (ok ? 0 : 1);
+    if (!ok || failed) return;
     merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
     WX_STAMP(3);
     WX_STAMP_RT(5);
@@ -1125,6 +1334,13 @@ template <int C, int VS, int W, int H>
 __global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
+}
+
+// Split segments: P workgroups (parts, one per CU) per segment, grid = S * P.
+template <int C, int VS, int W>
+__global__ __launch_bounds__(kWave*(W + 1)) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
+    AlignArgs a) {
+    align_dp_body<C, VS, W, 1, true>(a);
 }
 
 template <int C, int VS, int W, int H>
@@ -1648,10 +1864,40 @@ int buckets_for(int64_t min_N, int64_t max_N, int mode, int* ids) {
     return n;
 }
 
+// The split launch's one split bucket, for a batch whose longest segment has max_N tokens.
+int split_launch_id(int64_t max_N, int P) {
+    const int id = split_bucket_id((int)std::min<int64_t>(std::max<int64_t>(max_N, 1), 1 << 20), P);
+    if (id & kSplitFlag) return id;
+    int widest = 0;
+#define WX_WIDEST(CC, WW) widest = bucket_make(CC, WW, 1) | kSplitFlag;
+    WX_SPLIT_BUCKETS(WX_WIDEST)
+#undef WX_WIDEST
+    return widest;
+}
+
+// Kernels of a split launch: the split bucket, then the single-CU latency buckets of any
+// segment too long for it.
+int buckets_for_split(int64_t min_N, int64_t max_N, int P, int split_id, int* ids) {
+    int n = 0;
+    ids[n++] = split_id;
+    const int64_t cap = split_capacity_of(split_id, P);
+    const int C = bucket_C(split_id & ~kSplitFlag);
+    const int64_t small_hi = std::min<int64_t>(max_N, (int64_t)C * (C - 1));  // layout_fits holds above
+    if (C > 2 && min_N <= small_hi) n += buckets_for(min_N, small_hi, WX_MODE_THROUGHPUT, ids + n);
+    if (max_N > cap) n += buckets_for(std::max<int64_t>(min_N, cap + 1), max_N, WX_MODE_LATENCY, ids + n);
+    return n;
+}
+
+// bitmap words per block of the bucket `id` of an N-token segment in a launch of P parts
+int launch_cells_total(int id, int P) {
+    return (id & kSplitFlag) ? bucket_cells_total(id & ~kSplitFlag) * P : bucket_cells_total(id);
+}
+
 // bitmap: per segment (floor(row0/32) + seg) block offsets, 64 * C_stride dwords per block
 size_t bitmap_bytes(int32_t S, int64_t sum_T, int64_t max_N, int* stride_cells) {
-    const int nmax = (int)std::max<int64_t>(max_N, 1);  // widest bucket of either mode
-    const int cells = std::max(bucket_cells_total(bucket_id(nmax, 0)), bucket_cells_total(bucket_id(nmax, 1)));
+    const int nmax = (int)std::max<int64_t>(max_N, 1);  // widest bucket of any launch shape
+    int cells = std::max(bucket_cells_total(bucket_id(nmax, 0)), bucket_cells_total(bucket_id(nmax, 1)));
+    for (int P = 2; P <= kMaxParts; ++P) cells = std::max(cells, launch_cells_total(split_launch_id(nmax, P), P));
     if (stride_cells) *stride_cells = cells;
     const int64_t blocks = sum_T / kChunk + S + 1;
     return align_up((size_t)blocks * (size_t)cells * 4u, 256);
@@ -1678,7 +1924,8 @@ const char* wx_strerror(int code) {
 // Launch shape: latency buckets while the batch cannot fill the chip with one wave per
 // segment.  WX_ALIGN_MODE=0/1 forces a shape for WX_MODE_AUTO calls (benchmarking only).
 int align_mode(int32_t S, int32_t mode) {
-    if (mode == WX_MODE_THROUGHPUT || mode == WX_MODE_LATENCY) return mode;
+    if (mode == WX_MODE_THROUGHPUT) return mode;
+    if (mode != WX_MODE_AUTO) return WX_MODE_LATENCY;  // LATENCY, LATENCY_1CU, SPLIT2..4
     static const int forced = [] {
         const char* e = getenv("WX_ALIGN_MODE");
         return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : -1;
@@ -1692,9 +1939,48 @@ size_t cmask_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T / 
 // column N history: segment s at (row0 + 4 s) & ~3 (16-byte aligned groups of 8 rows)
 size_t cn_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T + 4 * (int64_t)S + 16) * 4u, 256); }
 
+// split hand-off granules: per (floor(row0/32) + seg + chunk) block, 3 boundaries x 40
+size_t xg_bytes(int32_t S, int64_t sum_T) {
+    return align_up((size_t)(sum_T / kChunk + S + 2) * (kMaxParts - 1) * kHaloCells * 8u, 256);
+}
+size_t arrive_bytes(int32_t S) { return align_up((size_t)(S + 1) * 4u, 256); }
+
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
     return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T) +
-           cn_bytes(S, sum_T);
+           cn_bytes(S, sum_T) + xg_bytes(S, sum_T) + arrive_bytes(S);
+}
+
+// CUs of the current device (cached per device).
+int device_cus() {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+// Parts per segment: latency launches split a segment over several CUs when the chip has
+// at least two CUs per segment.  WX_PARTS=1..4 overrides (benchmarking only).
+int split_parts(int32_t S, int mode, int32_t requested) {
+    static const int forced = [] {
+        const char* e = getenv("WX_PARTS");
+        return (e && e[0] >= '1' && e[0] <= '0' + kMaxParts) ? e[0] - '0' : 0;
+    }();
+    if (mode != WX_MODE_LATENCY) return 1;
+    if (requested == WX_MODE_LATENCY_1CU) return 1;
+    if (requested >= WX_MODE_SPLIT2 && requested <= WX_MODE_SPLIT4) return requested - WX_MODE_SPLIT2 + 2;
+    if (forced) return forced;
+    const int P = std::min(kMaxParts, device_cus() / std::max(S, 1));
+    return P >= 2 ? P : 1;
+}
+
+unsigned next_epoch() {
+    static std::atomic<unsigned> e{(unsigned)std::chrono::steady_clock::now().time_since_epoch().count()};
+    return (e.fetch_add(1) + 1) & 0xFFFFFu;
 }
 
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
@@ -1709,7 +1995,8 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
                      const int64_t* tok_off, const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N,
                      int64_t sum_T, int32_t* seg_start, int32_t* seg_end, double* seg_score, int32_t* t_start,
                      int32_t* status, void* workspace, size_t workspace_bytes, int32_t mode, void* stream) {
-    if (mode < WX_MODE_AUTO || mode > WX_MODE_LATENCY) return WX_E_INVALID;
+    if (!(mode >= WX_MODE_AUTO && mode <= WX_MODE_LATENCY_1CU) && !(mode >= WX_MODE_SPLIT2 && mode <= WX_MODE_SPLIT4))
+        return WX_E_INVALID;
     if (S < 0 || sum_T < 0 || min_N < 0 || max_N < min_N) return WX_E_INVALID;
     if (S == 0) return WX_OK;
     if (!em || !em_off || !tok_off || !blank_id || !seg_start || !seg_end || !seg_score || !t_start || !status ||
@@ -1727,13 +2014,28 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
     a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
                                           align_up((size_t)(sum_T + 1) * 4u, 256));
     a.cn = reinterpret_cast<float*>(reinterpret_cast<char*>(a.cmask) + cmask_bytes(S, sum_T));
+    a.xg = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
+    a.arrive = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.xg) + xg_bytes(S, sum_T));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a.mode = align_mode(S, mode);
+    a.parts = split_parts(S, a.mode, mode);
+    a.epoch = next_epoch();
     a.x4 = (V == 32 && (reinterpret_cast<uintptr_t>(em) & 15) == 0) ? 1 : 0;
-    int ids[kNumBuckets];
-    const int n = buckets_for(min_N, max_N, a.mode, ids);
+    int ids[kNumBuckets + 8];
+    a.split_id = a.parts > 1 ? split_launch_id(max_N, a.parts) : 0;
+    const int n = a.parts > 1 ? buckets_for_split(min_N, max_N, a.parts, a.split_id, ids)
+                              : buckets_for(min_N, max_N, a.mode, ids);
     const dim3 grid(S);
     return fork_join(st, n, [&](int i, hipStream_t s) {
+#define WX_LAUNCH_SPLIT(CC, WW)                                                                        \
+        if (ids[i] == (bucket_make(CC, WW, 1) | kSplitFlag)) {                                          \
+            const dim3 g2((unsigned)S * (unsigned)a.parts), b2(kWave * (WW + 1));                       \
+            if (V <= 32) hipLaunchKernelGGL((align_dp_split_kernel<CC, 32, WW>), g2, b2, 0, s, a);       \
+            else if (V <= 64) hipLaunchKernelGGL((align_dp_split_kernel<CC, 64, WW>), g2, b2, 0, s, a);  \
+            else hipLaunchKernelGGL((align_dp_split_kernel<CC, kGatherVS, WW>), g2, b2, 0, s, a);        \
+        }
+        WX_SPLIT_BUCKETS(WX_LAUNCH_SPLIT)
+#undef WX_LAUNCH_SPLIT
 #define WX_LAUNCH_ALIGN(CC, WW, HH)                                                                  \
         if (ids[i] == bucket_make(CC, WW, HH)) {                                                       \
             if (V <= 32) launch_align_dp<CC, 32, WW, HH>(grid, s, a);                                  \
