@@ -286,7 +286,8 @@ def main():
         B = algorithmic_bytes(batch.Ts, batch.Ns, V)
         launch_s = time_steps.last_launch_s  # HIP events around each step's kernel
         achieved = B / launch_s / 1e9
-        kname = f"void wx::align_dp_kernel<2, {32 if V <= 32 else 64}, 7, 1>(wx::AlignArgs)"
+        knames = _lib.align_dp_plan(batch.S, batch.min_N, batch.max_N, V)  # kernels this step launches
+        kname = knames[0] if knames else "?"
         traffic, traffic_src = pmc_traffic(kname)
         out = {
             "metric": "aligned audio-sec/s + word-boundary MAE(ms) vs ref, 1/2/4/8 GPU",
@@ -307,8 +308,8 @@ def main():
                        "parallelism": f"dp{world} (per-file sharding, RCCL vocab broadcast)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "align_dp_kernel<2,32,7,1> (the step's only launch: all 64 segments, "
-                                   "N 257..704 bucket)",
+                         "kernel": kname + (" (the step's only launch)" if len(knames) == 1 else
+                                            f" (+{len(knames) - 1} more launches)"),
                          "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6},
         }
         mae, ntok, nbad = mae_vs_oracle([e.cpu().numpy() for e in ems], toks, plan)
@@ -346,6 +347,35 @@ def main():
                                         "achieved_GBps": B3 / (d3 / 3) / 1e9,
                                         "frac": B3 / (d3 / 3) / 1e9 / HBM_PEAK_GBPS,
                                         "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b3.Ts, b3.Ns))) / (d3 / 3)}
+            # get_trellis (materialised, wx_trellis) on the same T=3000 batch: the HBM-write-bound
+            # kernel of the path (4 B per cell written)
+            try:
+                tr_flat, tr_offs = _lib.trellis(b3)
+                tr_off_d = _lib._dev_i64(tr_offs, device)
+                lib = _lib.load()
+
+                def tr_run():
+                    lib.wx_trellis(_lib._ptr(b3.em), _lib._ptr(b3.em_off_d), b3.V, _lib._ptr(b3.tok),
+                                   _lib._ptr(b3.tok_off_d), _lib._ptr(b3.blank), b3.S, b3.max_N, _lib._ptr(tr_flat),
+                                   _lib._ptr(tr_off_d), _lib._stream(device))
+                tr_run()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    tr_run()
+                e1.record()
+                torch.cuda.synchronize()
+                dt = e0.elapsed_time(e1) / 1000.0 / 3
+                Bt = sum(4 * t_ * V + 4 * n_ + 4 * (t_ + 1) * (n_ + 1) for t_, n_ in zip(b3.Ts, b3.Ns))
+                extra["trellis_T3000"] = {"kernel": "wx_trellis (get_trellis, materialised fp32 [T+1,N+1])",
+                                          "segments": n3, "ms_per_launch": 1000 * dt,
+                                          "bytes_per_launch": Bt, "achieved_GBps": Bt / dt / 1e9,
+                                          "frac": Bt / dt / 1e9 / HBM_PEAK_GBPS,
+                                          "bytes_per_cell": 4, "bound": "hbm (writes)"}
+                del tr_flat
+            except Exception as e:  # never let the secondary leg hide the primary line
+                extra["trellis_T3000"] = {"error": repr(e)[:200]}
             del p3, b3
             torch.cuda.empty_cache()
         if not args.no_cpu and world == 1:

@@ -108,16 +108,17 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
  *   WX_MODE_AUTO        latency shape for batches of <= 256 segments, else throughput;
  *   WX_MODE_THROUGHPUT  one wave per segment up to 2048 tokens (most segments in flight);
  *   WX_MODE_LATENCY     each segment's columns spread over up to 8 waves (shortest time
- *                       per segment when the batch cannot fill the GPU); when the device
- *                       has >= 2 CUs per segment, over up to 4 CUs (split parts).
+ *                       per segment when the batch cannot fill the GPU), one CU each;
+ *   WX_MODE_SPLIT2..4   the latency shape with each segment spread over 2..4 CUs (capped
+ *                       at the device's CUs / S; slightly faster, 4x the emission reads).
  * wx_align_dp == wx_align_dp_mode(..., WX_MODE_AUTO) unless the environment variable
- * WX_ALIGN_MODE=0/1 forces a shape (benchmarking); WX_PARTS=1..4 forces the parts per
- * segment of latency launches. */
+ * WX_ALIGN_MODE=0/1 forces a shape (benchmarking); WX_PARTS=2..4 opts latency launches
+ * into the split. */
 enum {
     WX_MODE_AUTO = -1,
     WX_MODE_THROUGHPUT = 0,
-    WX_MODE_LATENCY = 1,     /* parts per segment chosen from the device's CU count */
-    WX_MODE_LATENCY_1CU = 2, /* latency shape, one CU per segment */
+    WX_MODE_LATENCY = 1,     /* one CU per segment (WX_PARTS=2..4: split) */
+    WX_MODE_LATENCY_1CU = 2, /* latency shape, one CU per segment, whatever WX_PARTS says */
     WX_MODE_SPLIT2 = 12,     /* latency shape, 2 / 3 / 4 CUs per segment */
     WX_MODE_SPLIT3 = 13,
     WX_MODE_SPLIT4 = 14
@@ -128,6 +129,11 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V,
                      int32_t* seg_start, int32_t* seg_end, double* seg_score,
                      int32_t* t_start, int32_t* status,
                      void* workspace, size_t workspace_bytes, int32_t mode, void* stream);
+
+/* Diagnostics (no device work): the kernels wx_align_dp_mode would launch for a batch of S
+ * segments with token counts in [min_N, max_N] and vocabulary size V, written to buf as a
+ * ';'-separated list of their rocprof names (truncated to n bytes).  Returns their number. */
+int wx_align_dp_plan(int32_t S, int64_t min_N, int64_t max_N, int32_t V, int32_t mode, char* buf, size_t n);
 
 /* Binarize.__call__ (vad.py:118-180) for n_files score columns (CSR by f_off) with
  * pyannote sliding-window geometry per file (frame i is centred at

@@ -71,6 +71,28 @@ def test_argument_validation_without_device(lib):
                            None) == 1001
 
 
+def test_launch_plan_bucket_selection(lib):
+    """Host-side launch planning (wx_align_dp_plan, no device work): the kernels a batch maps
+    to in each launch shape."""
+    from whisperx_amd import _lib
+
+    k = "void wx::align_dp_kernel<{}>(wx::AlignArgs)".format
+    sk = "void wx::align_dp_split_kernel<{}>(wx::AlignArgs)".format
+    # config 2 (64 x 30 s, N 300..500): one latency launch, one CU per segment
+    assert _lib.align_dp_plan(64, 300, 500, 32) == [k("2, 32, 7, 1")]
+    assert _lib.align_dp_plan(64, 300, 500, 32, _lib.MODE_LATENCY_1CU) == [k("2, 32, 7, 1")]
+    # split over 4 CUs: one split kernel for the whole batch (the bucket of its longest segment)
+    assert _lib.align_dp_plan(64, 300, 500, 32, _lib.MODE_SPLIT4) == [sk("1, 32, 4")]
+    assert _lib.align_dp_plan(64, 300, 1100, 32, _lib.MODE_SPLIT4) == [sk("2, 32, 3")]
+    # ... short segments a wide split bucket cannot lay out take throughput buckets beside it
+    assert _lib.align_dp_plan(64, 1, 2000, 32, _lib.MODE_SPLIT4) == [sk("4, 32, 3"), k("1, 32, 1, 0")]
+    # saturated batches: throughput buckets by N; V picks the LDS row width (32 / 64 / gather)
+    assert _lib.align_dp_plan(4096, 300, 500, 32) == [k("6, 32, 1, 0"), k("8, 32, 1, 0")]
+    assert _lib.align_dp_plan(2048, 850, 951, 40) == [k("8, 64, 2, 0")]
+    assert _lib.align_dp_plan(2048, 850, 951, 1000) == [k("8, 256, 2, 0")]
+    assert _lib.align_dp_plan(0, 1, 1, 32) == []
+
+
 def test_product_refuses_without_device():
     import torch
 

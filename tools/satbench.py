@@ -134,6 +134,10 @@ def child(args):
             lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)
             out[case]["loop_med_per_wave"] = [[float(np.median(lp[:, w, i])) for i in range(3)] for w in range(8)
                                               if lp[:, w, 0].max() > 0]
+            wk = lp[:, 15, :]
+            wk = wk[wk[:, 1] > 0]
+            if len(wk):
+                out[case]["walk_split_med(argmax,walk,compact)"] = [float(np.median(wk[:, i])) for i in range(3)]
             rt = (ph[:, 5] - ph[:, 4]) / 100.0  # s_memrealtime ticks at 100 MHz -> us
             out[case]["seg_us_med"] = float(np.median(rt))
             ent = (ph[:, 4] - ph[:, 4].min()) / 100.0
@@ -175,7 +179,7 @@ def main():
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
                 for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
-                          "loop_med_per_wave"):
+                          "loop_med_per_wave", "walk_split_med(argmax,walk,compact)"):
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)
     libs = list(results)

@@ -45,6 +45,7 @@ SIGNATURES = {
                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "wx_align_dp_mode": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _sz, _i32, _vp]),
+    "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
 }
@@ -238,6 +239,14 @@ class AlignPlan:
         st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.b.device).cuda_stream)
         _check(self.lib.wx_align_dp_mode(*self.args, self.mode, st))
         return self.seg_start, self.seg_end, self.seg_score, self.t_start, self.status
+
+
+def align_dp_plan(S: int, min_N: int, max_N: int, V: int, mode: int = MODE_AUTO):
+    """Kernel names (rocprof form) wx_align_dp_mode launches for such a batch."""
+    lib = load(require_device=False)
+    buf = ctypes.create_string_buffer(4096)
+    lib.wx_align_dp_plan(S, min_N, max_N, V, mode, buf, len(buf))
+    return [x for x in buf.value.decode().split(";") if x]
 
 
 def trellis(b: Batch):

@@ -33,7 +33,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <atomic>
@@ -541,8 +543,8 @@ struct Forward {
         const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
 
         if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
-        uint64_t xpre[C];           // SP: granules of the next chunk's halo (prefetched)
-        bool xlost = false;         // SP: a hand-off timed out
+        uint64_t xpre[C];    // SP: the next chunk's halo granules (prefetched one chunk ahead)
+        bool xlost = false;  // SP: a hand-off timed out
 #pragma unroll
         for (int k = 0; k < C; ++k) xpre[k] = 0;
         if (SP && xsub && nch > 1 && l < Geo::HL) {
@@ -578,24 +580,26 @@ struct Forward {
                 // Halo of row 32q from the previous part: the granules prefetched one chunk
                 // ago.  A part must trail its predecessor by more than a chunk plus the
                 // hand-off latency for the prefetch to find them; at chunk 1, and after any
-                // miss, it therefore also waits for the next chunk's granules (re-building
-                // that slack once instead of paying a round trip every chunk).  Waits are
-                // bounded: a lost hand-off marks the segment failed instead of hanging.
+                // miss, it therefore also waits until chunk q + kXSlack is visible
+                // (re-building that slack once instead of paying a round trip every chunk).
+                // Waits are bounded: a lost hand-off marks the segment failed.  (Measured no
+                // better: a two-deep prefetch in registers — hipcc's waitcnt pass drains both
+                // sets — and an LDS-DMA landing ring with hand-counted vmcnt.)
                 const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost);
                 if (l < Geo::HL) {
 #pragma unroll
                     for (int k = 0; k < C; ++k) st.cur[k] = __builtin_bit_cast(float, (unsigned)xpre[k]);
                 }
-                if ((missed || q == 1) && q + kXSlack < nch) {  // (re)build the slack
+                if ((missed || q == 1) && q + kXSlack < nch) {
                     uint64_t tmp[C];
 #pragma unroll
                     for (int k = 0; k < C; ++k) tmp[k] = 0;
                     xwait(sp->xin, sp->xstride, q + kXSlack, l, sp->tag, tmp, xlost);
                 }
                 if (q + 1 < nch && l < Geo::HL) {
-                    const uint64_t* gn = sp->xin + (int64_t)(q + 1) * sp->xstride + l * C;
 #pragma unroll
-                    for (int k = 0; k < C; ++k) xpre[k] = granule_load(gn + k);
+                    for (int k = 0; k < C; ++k)
+                        xpre[k] = granule_load(sp->xin + (int64_t)(q + 1) * sp->xstride + l * C + k);
                 }
             }
             if (!H) {
@@ -847,8 +851,12 @@ struct Forward {
         const float(&et)[C] = rw.et;
         // last cell of the lane to the left (short lanes end at slot C-2)
         const float src = (C > 1 && is_short) ? st.cur[C > 1 ? C - 2 : 0] : st.cur[C - 1];
-        const float in0 = COL == 3 ? rw.c0 : (COL ? st.col0 : src);
-        const float left = dpp_shr1(in0, src);
+        // Lane 0's left input is column 0 in the column-1 wave and a halo lane's don't-care
+        // elsewhere: there the DPP zero-fills (bound_ctrl), which saves the v_mov that sets
+        // up the `old` operand on the step's dependency chain.
+        const float left = COL ? dpp_shr1(COL == 3 ? rw.c0 : st.col0, src)
+                               : __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src),
+                                                                                    0x138, 0xF, 0xF, true));
 #pragma unroll
         for (int k = C - 1; k >= 0; --k) {
             const float s = st.cur[k] + eb;
@@ -980,24 +988,63 @@ __device__ __forceinline__ unsigned walk_block(unsigned win, int& d) {
     return cm;
 }
 
+// Run-length form of walk_block: one iteration per token change instead of per step.
+// The path stays on window lane d until the next set bit (in walking order: increasing
+// bit position) of that lane's word, moves there, and continues from the next step on
+// lane d+1.  A successful path makes exactly N changes, so the serial chain costs
+// ~N * (readlane + 8 SALU) per segment instead of T * 4 SALU + the ballot transposes.
+// Same contract as walk_block: bits of steps before the walk's start are cleared.
+__device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
+    // Per change: x = word[dd] & m (m: bit positions still ahead); low = x & -x is the
+    // change; m = -(low << 1) keeps the positions after it (0 after bit 31: the loop ends
+    // and dd <= 64 is never read).  Hand-scheduled: 9 scalar-unit instructions per change
+    // (hipcc's version of the same loop took 15).
+    unsigned cm = 0u, m = 0xFFFFFFFFu, w, t;
+    int dd = d;
+    asm volatile(
+        "v_readlane_b32 %[w], %[win], %[dd]\n\t"
+        "s_and_b32 %[w], %[w], %[m]\n\t"
+        "s_cbranch_scc0 2f\n"
+        "1:\n\t"
+        "s_sub_u32 %[t], 0, %[w]\n\t"
+        "s_and_b32 %[w], %[w], %[t]\n\t"
+        "s_or_b32 %[cm], %[cm], %[w]\n\t"
+        "s_lshl_b32 %[w], %[w], 1\n\t"
+        "s_sub_u32 %[m], 0, %[w]\n\t"
+        "s_add_u32 %[dd], %[dd], 1\n\t"
+        "v_readlane_b32 %[w], %[win], %[dd]\n\t"
+        "s_and_b32 %[w], %[w], %[m]\n\t"
+        "s_cbranch_scc1 1b\n"
+        "2:"
+        : [dd] "+s"(dd), [cm] "+s"(cm), [m] "+s"(m), [w] "=&s"(w), [t] "=&s"(t)
+        : [win] "v"(win)
+        : "scc");
+    d = dd;
+    return cm;
+}
+
 // The backtrack walk (alignment.py:395-421) over the decision bitmap: from (t_start, N),
 // step back one frame at a time and move to the previous token where the decision bit is
 // set.  Once j reaches 0 the window reads cell 0 (all zero), so blocks run to completion
 // without an early-exit test.  Per block only the change mask is kept (cmask[b]);
 // start frames are compacted from it afterwards.  Returns the lowest block touched, or -1
 // where the reference returns None.
-template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
-__device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask) {
+template <class LoadWin>  // LoadWin(b, A): this lane's word of window column A - lane in block b
+__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask) {
     if (t_start <= 0 || N <= 0) return -1;
     int j = N;
     int b = (t_start - 1) >> 5;
     int A = j;
     const int s_hi = (t_start - 1) & 31;  // steps above t_start-1 do not exist: clear their bits
-    unsigned win = load_window<CC>(bits, lay, b, A) & (0xFFFFFFFFu << (31 - s_hi));
+    unsigned win = load_win(b, A) & (0xFFFFFFFFu << (31 - s_hi));
     int An = A;
-    unsigned nxt = (b > 0) ? load_window<CC>(bits, lay, b - 1, An) : 0u;
+    unsigned nxt = (b > 0) ? load_win(b - 1, An) : 0u;
     int d = 0;
+#ifdef WX_WALK_BALLOT
     unsigned cm = walk_block(win, d);
+#else
+    unsigned cm = walk_block_rl(win, d);
+#endif
     while (true) {
         cmask[b] = cm;
         j = uniform(A - d);
@@ -1007,10 +1054,19 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
         win = nxt;
         A = An;
         An = j;
-        nxt = (b > 0) ? load_window<CC>(bits, lay, b - 1, An) : 0u;
+        nxt = (b > 0) ? load_win(b - 1, An) : 0u;
         d = A - j;
+#ifdef WX_WALK_BALLOT
         cm = walk_block(win, d);
+#else
+        cm = walk_block_rl(win, d);
+#endif
     }
+}
+
+template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
+__device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask) {
+    return walk_impl([&](int b, int A) { return load_window<CC>(bits, lay, b, A); }, N, t_start, cmask);
 }
 
 // start[k] = k-th change frame in increasing time: a popcount prefix over the change masks
@@ -1302,19 +1358,37 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         __syncthreads();
     }
     int32_t* start = a.seg_start + d.tok0;
+#ifdef WX_PHASE_TIMING
+    WX_T(w0);
+#endif
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
         const int ts = column_argmax(cn, d.T);
+#ifdef WX_PHASE_TIMING
+        WX_T(w1);
+#endif
         if (lane == 0) {
             a.t_start[seg] = ts;
             tsb[0] = ts;
         }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
         const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W * P), d.N, ts, cmask);
+#ifdef WX_PHASE_TIMING
+        WX_T(w2);
+#endif
         if (b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
         }
         if (lane == 0) tsb[1] = b_lo >= 0 ? 1 : 0;
+#ifdef WX_PHASE_TIMING
+        WX_T(w3);
+        if (lane == 0 && blockIdx.x < 8192) {  // walk-phase split: argmax, walk, compaction
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + 15) * 3;
+            o[0] = w1 - w0;
+            o[1] = w2 - w1;
+            o[2] = w3 - w2;
+        }
+#endif
     } else if (H) {
         fill_q0(E, a.V, d.T, q0, kWave);
     }
@@ -1963,8 +2037,12 @@ int device_cus() {
     return cache[dev];
 }
 
-// Parts per segment: latency launches split a segment over several CUs when the chip has
-// at least two CUs per segment.  WX_PARTS=1..4 overrides (benchmarking only).
+// Parts per segment of a latency launch: one CU per segment unless a split mode is asked for
+// (WX_MODE_SPLIT2..4, or WX_PARTS=2..4 for WX_MODE_AUTO / WX_MODE_LATENCY calls).  Measured on
+// config 2 (64 x T=1499): 4 parts are 3-4% faster than one CU (steps 58 vs 83 cycles, but the
+// cross-CU hand-offs add ~30 cycles per step) while every part stages all emission rows (4.4x
+// the fabric traffic), so the split is opt-in.  The CU count caps the parts: every part of
+// every segment must be resident at once.
 int split_parts(int32_t S, int mode, int32_t requested) {
     static const int forced = [] {
         const char* e = getenv("WX_PARTS");
@@ -1972,10 +2050,14 @@ int split_parts(int32_t S, int mode, int32_t requested) {
     }();
     if (mode != WX_MODE_LATENCY) return 1;
     if (requested == WX_MODE_LATENCY_1CU) return 1;
-    if (requested >= WX_MODE_SPLIT2 && requested <= WX_MODE_SPLIT4) return requested - WX_MODE_SPLIT2 + 2;
-    if (forced) return forced;
-    const int P = std::min(kMaxParts, device_cus() / std::max(S, 1));
-    return P >= 2 ? P : 1;
+    int want = 1;
+    if (requested >= WX_MODE_SPLIT2 && requested <= WX_MODE_SPLIT4)
+        want = requested - WX_MODE_SPLIT2 + 2;
+    else if (forced)
+        want = forced;
+    if (want <= 1) return 1;
+    const int fit = device_cus() / std::max(S, 1);
+    return std::max(1, std::min(want, fit)) >= 2 ? std::max(1, std::min(want, fit)) : 1;
 }
 
 unsigned next_epoch() {
@@ -2045,6 +2127,32 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
         WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
     });
+}
+
+int wx_align_dp_plan(int32_t S, int64_t min_N, int64_t max_N, int32_t V, int32_t mode, char* buf, size_t n) {
+    if (S <= 0 || min_N < 0 || max_N < min_N || V < 1) return 0;
+    const int m = align_mode(S, mode);
+    const int P = split_parts(S, m, mode);
+    int ids[kNumBuckets + 8];
+    const int cnt = P > 1 ? buckets_for_split(min_N, max_N, P, split_launch_id(max_N, P), ids)
+                          : buckets_for(min_N, max_N, m, ids);
+    const int vs = V <= 32 ? 32 : (V <= 64 ? 64 : kGatherVS);
+    size_t used = 0;
+    for (int i = 0; i < cnt && buf && n > 0; ++i) {
+        const int id = ids[i] & ~kSplitFlag;
+        char one[160];
+        if (ids[i] & kSplitFlag)
+            snprintf(one, sizeof one, "%svoid wx::align_dp_split_kernel<%d, %d, %d>(wx::AlignArgs)", i ? ";" : "",
+                     bucket_C(id), vs, bucket_W(id));
+        else
+            snprintf(one, sizeof one, "%svoid wx::align_dp_kernel<%d, %d, %d, %d>(wx::AlignArgs)", i ? ";" : "",
+                     bucket_C(id), vs, bucket_W(id), id & 1);
+        const size_t len = strlen(one);
+        if (used + len + 1 > n) break;
+        memcpy(buf + used, one, len + 1);
+        used += len;
+    }
+    return cnt;
 }
 
 int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
