@@ -852,11 +852,20 @@ struct Forward {
         // last cell of the lane to the left (short lanes end at slot C-2)
         const float src = (C > 1 && is_short) ? st.cur[C > 1 ? C - 2 : 0] : st.cur[C - 1];
         // Lane 0's left input is column 0 in the column-1 wave and a halo lane's don't-care
-        // elsewhere: there the DPP zero-fills (bound_ctrl), which saves the v_mov that sets
-        // up the `old` operand on the step's dependency chain.
-        const float left = COL ? dpp_shr1(COL == 3 ? rw.c0 : st.col0, src)
-                               : __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src),
-                                                                                    0x138, 0xF, 0xF, true));
+        // elsewhere: there the DPP zero-fills (bound_ctrl).  In the column-1 wave lane 63
+        // passes column 0 round to lane 0 instead (wave_ror:1; lane 63's own last cell feeds
+        // no lane of this wave).  Either way every lane's source is a plain register, so
+        // hipcc fuses the shift into the add (v_add_f32_dpp) and no v_mov sets up `old`.
+        float left;
+        if (COL) {
+            const float c0v = COL == 3 ? rw.c0 : st.col0;
+            const float src2 = lane_id() == kWave - 1 ? c0v : src;
+            left = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src2), 0x13C /* wave_ror:1 */,
+                                                                      0xF, 0xF, true));  // (no lane is out of range)
+        } else {
+            left = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src), 0x138 /* wave_shr:1 */,
+                                                                      0xF, 0xF, true));
+        }
 #pragma unroll
         for (int k = C - 1; k >= 0; --k) {
             const float s = st.cur[k] + eb;
