@@ -20,6 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = {  # name: (segments, T, N range)
     "b64": (64, 1499, (300, 500)),
+    "b16": (16, 1499, (300, 500)),
+    "b32": (32, 1499, (300, 500)),
+    "b128": (128, 1499, (300, 500)),
+    "b64n900": (64, 2999, (850, 951)),
     "sat1499": (4096, 1499, (300, 500)),
     "sat3000": (2048, 2999, (850, 951)),
     "sat3000_1024": (1024, 2999, (850, 951)),
@@ -134,6 +138,10 @@ def child(args):
             lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)
             out[case]["loop_med_per_wave"] = [[float(np.median(lp[:, w, i])) for i in range(3)] for w in range(8)
                                               if lp[:, w, 0].max() > 0]
+            xk = lp[:, 14, :]
+            xk = xk[xk[:, 1] > 0]
+            if len(xk):
+                out[case]["handoff_med(misses,wait_cyc,slack_cyc)"] = [float(np.median(xk[:, i])) for i in range(3)]
             wk = lp[:, 15, :]
             wk = wk[wk[:, 1] > 0]
             if len(wk):
@@ -179,7 +187,8 @@ def main():
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
                 for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
-                          "loop_med_per_wave", "walk_split_med(argmax,walk,compact)"):
+                          "loop_med_per_wave", "walk_split_med(argmax,walk,compact)",
+                          "handoff_med(misses,wait_cyc,slack_cyc)"):
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)
     libs = list(results)

@@ -350,16 +350,16 @@ __device__ unsigned long long wx_loop[8192 * 16 * 3];
 // the previous part's wave W-1, handed over once per 32-row chunk through global memory
 // as 8-byte {value, tag} granules (one sc1 store each; the tag carries the launch epoch and
 // the chunk, so a granule is valid on its own — no flag, no fence).  A part lags its
-// predecessor by about one chunk plus the hand-off latency; the consumer prefetches the
-// next chunk's granules one chunk ahead.  Each part then arrives at a per-segment counter;
+// predecessor by a few chunks; the consumer prefetches each chunk's granules two chunks
+// ahead.  Each part then arrives at a per-segment counter;
 // the last to arrive runs the argmax, the walk and merge_repeats.
 constexpr int kMaxParts = 4;
 constexpr int kHaloCells = 40;  // >= HL * C = ceil(32 / C) * C for every C
 constexpr int kMaxSpin = 1 << 16;
 #ifndef WX_XSLACK
-#define WX_XSLACK 2
+#define WX_XSLACK 3
 #endif
-constexpr int kXSlack = WX_XSLACK;  // chunks a part trails its predecessor by (>= 1)  // granule re-reads (~1 us each) before a hand-off counts as lost
+constexpr int kXSlack = WX_XSLACK;  // chunks a part trails its predecessor by (>= 3)
 
 struct Split {
     int p, P;         // this part, parts per segment
@@ -543,18 +543,24 @@ struct Forward {
         const int inf_from = T + 1 - N;  // rows >= inf_from have column 0 = +inf
 
         if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
-        uint64_t xpre[C];    // SP: the next chunk's halo granules (prefetched one chunk ahead)
+        // SP: halo granules prefetched two chunks ahead, odd chunks in xodd, even in xeven.
+        // The chunk loop is unrolled by two for split launches so that each set stays in its
+        // own registers (a loop-carried swap would make hipcc wait for both loads).
+        uint64_t xodd[C], xeven[C];
         bool xlost = false;  // SP: a hand-off timed out
 #pragma unroll
-        for (int k = 0; k < C; ++k) xpre[k] = 0;
-        if (SP && xsub && nch > 1 && l < Geo::HL) {
+        for (int k = 0; k < C; ++k) xodd[k] = xeven[k] = 0;
+        if (SP && xsub && l < Geo::HL) {
 #pragma unroll
-            for (int k = 0; k < C; ++k) xpre[k] = granule_load(sp->xin + sp->xstride + l * C + k);
+            for (int k = 0; k < C; ++k) {
+                if (nch > 1) xodd[k] = granule_load(sp->xin + sp->xstride + l * C + k);
+                if (nch > 2) xeven[k] = granule_load(sp->xin + 2 * sp->xstride + l * C + k);
+            }
         }
 #ifdef WX_PHASE_TIMING
-        unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0;
+        unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0, x_miss = 0, x_wait = 0, x_slack = 0;
 #endif
-        for (int q = 0; q < nch; ++q) {
+        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C]) {
             WX_T(c0);
             float* buf = lds + (q % kBufs) * kChunk * VS;
             const int rows = min(kChunk, T - q * kChunk);
@@ -577,29 +583,37 @@ struct Forward {
                 for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
             }
             if (SP && xsub && q > 0) {
-                // Halo of row 32q from the previous part: the granules prefetched one chunk
-                // ago.  A part must trail its predecessor by more than a chunk plus the
-                // hand-off latency for the prefetch to find them; at chunk 1, and after any
-                // miss, it therefore also waits until chunk q + kXSlack is visible
-                // (re-building that slack once instead of paying a round trip every chunk).
-                // Waits are bounded: a lost hand-off marks the segment failed.  (Measured no
-                // better: a two-deep prefetch in registers — hipcc's waitcnt pass drains both
-                // sets — and an LDS-DMA landing ring with hand-counted vmcnt.)
+                // Halo of row 32q from the previous part: the granules prefetched two chunks
+                // ago (the sc1 load takes longer than a chunk).  A part must trail its
+                // predecessor by more than the prefetch distance plus the hand-off latency for
+                // the prefetch to find them; at chunk 1, and after any miss, it therefore also
+                // waits until chunk q + kXSlack is visible (re-building that slack once instead
+                // of paying a round trip every chunk).  Waits are bounded: a lost hand-off
+                // marks the segment failed.  (An LDS-DMA landing ring with hand-counted vmcnt
+                // measured no better.)
+                WX_T(x0);
                 const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost);
                 if (l < Geo::HL) {
 #pragma unroll
                     for (int k = 0; k < C; ++k) st.cur[k] = __builtin_bit_cast(float, (unsigned)xpre[k]);
                 }
+                WX_T(x1);
                 if ((missed || q == 1) && q + kXSlack < nch) {
                     uint64_t tmp[C];
 #pragma unroll
                     for (int k = 0; k < C; ++k) tmp[k] = 0;
                     xwait(sp->xin, sp->xstride, q + kXSlack, l, sp->tag, tmp, xlost);
                 }
-                if (q + 1 < nch && l < Geo::HL) {
+#ifdef WX_PHASE_TIMING
+                WX_T(x2);
+                x_miss += missed ? 1 : 0;
+                x_wait += x1 - x0;
+                x_slack += x2 - x1;
+#endif
+                if (q + 2 < nch && l < Geo::HL) {  // this set's next chunk: q + 2
 #pragma unroll
                     for (int k = 0; k < C; ++k)
-                        xpre[k] = granule_load(sp->xin + (int64_t)(q + 1) * sp->xstride + l * C + k);
+                        xpre[k] = granule_load(sp->xin + (int64_t)(q + 2) * sp->xstride + l * C + k);
                 }
             }
             if (!H) {
@@ -629,6 +643,14 @@ struct Forward {
                     st.w[k] = 0u;
                 }
             }
+        };
+        if constexpr (SP) {
+            for (int q = 0; q < nch; q += 2) {
+                chunk_iter(q, xeven);
+                if (q + 1 < nch) chunk_iter(q + 1, xodd);
+            }
+        } else {
+            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven);
         }
 #ifdef WX_PHASE_TIMING
         if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
@@ -636,6 +658,12 @@ struct Forward {
             o[0] = acc_steps;
             o[1] = acc_bar;
             o[2] = acc_other;
+            if (SP && xsub) {  // hand-off: missed prefetches, cycles in the chunk's wait, in slack waits
+                unsigned long long* x = wx_loop + ((size_t)blockIdx.x * 16 + 14) * 3;
+                x[0] = x_miss;
+                x[1] = x_wait;
+                x[2] = x_slack;
+            }
         }
 #endif
         return xlost;
