@@ -105,12 +105,13 @@ int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
                 void* workspace, size_t workspace_bytes, void* stream);
 
 /* wx_align_dp with an explicit launch shape (results are identical in every mode):
- *   WX_MODE_AUTO        latency shape for batches of <= 256 segments, else throughput;
+ *   WX_MODE_AUTO        latency shape for batches of <= 256 segments (split over 4 CUs per
+ *                       segment when the device has 4 CUs per segment), else throughput;
  *   WX_MODE_THROUGHPUT  one wave per segment up to 2048 tokens (most segments in flight);
  *   WX_MODE_LATENCY     each segment's columns spread over up to 8 waves (shortest time
  *                       per segment when the batch cannot fill the GPU), one CU each;
  *   WX_MODE_SPLIT2..4   the latency shape with each segment spread over 2..4 CUs (capped
- *                       at the device's CUs / S; slightly faster, 4x the emission reads).
+ *                       at the device's CUs / S; 4x the emission reads).
  * wx_align_dp == wx_align_dp_mode(..., WX_MODE_AUTO) unless the environment variable
  * WX_ALIGN_MODE=0/1 forces a shape (benchmarking); WX_PARTS=2..4 opts latency launches
  * into the split. */

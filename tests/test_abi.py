@@ -78,8 +78,11 @@ def test_launch_plan_bucket_selection(lib):
 
     k = "void wx::align_dp_kernel<{}>(wx::AlignArgs)".format
     sk = "void wx::align_dp_split_kernel<{}>(wx::AlignArgs)".format
-    # config 2 (64 x 30 s, N 300..500): one latency launch, one CU per segment
-    assert _lib.align_dp_plan(64, 300, 500, 32) == [k("2, 32, 7, 1")]
+    # config 2 (64 x 30 s, N 300..500): one latency launch, each segment over 4 CUs (the
+    # planner assumes 256 CUs without a device); 128 segments: one CU per segment
+    assert _lib.align_dp_plan(64, 300, 500, 32) == [sk("1, 32, 4")]
+    assert _lib.align_dp_plan(128, 300, 500, 32) == [k("2, 32, 7, 1")]
+    assert _lib.align_dp_plan(64, 300, 500, 32, _lib.MODE_LATENCY) == [k("2, 32, 7, 1")]
     assert _lib.align_dp_plan(64, 300, 500, 32, _lib.MODE_LATENCY_1CU) == [k("2, 32, 7, 1")]
     # split over 4 CUs: one split kernel for the whole batch (the bucket of its longest segment)
     assert _lib.align_dp_plan(64, 300, 500, 32, _lib.MODE_SPLIT4) == [sk("1, 32, 4")]

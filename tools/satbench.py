@@ -120,6 +120,11 @@ def child(args):
             buf = (ctypes.c_ulonglong * (6 * n))()
             lib.wx_debug_phases(buf, n)
             ph = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)
+            # split grids: block ((s // 8) * P + p) * 8 + s % 8 -> row s * P + p (S % 8 == 0)
+            P = args.parts
+            perm = np.array([((s // 8) * P + q) * 8 + s % 8 for s in range(n // P) for q in range(P)]) \
+                if P > 1 else np.arange(n)
+            ph = ph[perm]
             fwd, walk, mrg = ph[:, 1] - ph[:, 0], ph[:, 2] - ph[:, 1], ph[:, 3] - ph[:, 2]
             if args.parts > 1:
                 pf = fwd.reshape(-1, args.parts)
@@ -135,9 +140,16 @@ def child(args):
                                            "walk_max": float(walk.max()), "fwd_max": float(fwd.max())}
             lbuf = (ctypes.c_ulonglong * (n * 16 * 3))()
             lib.wx_debug_loop(lbuf, n)
-            lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)
+            lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)[perm]
             out[case]["loop_med_per_wave"] = [[float(np.median(lp[:, w, i])) for i in range(3)] for w in range(8)
                                               if lp[:, w, 0].max() > 0]
+            if args.parts > 1:
+                lq = lp.reshape(-1, args.parts, 16, 3)
+                out[case]["loop_med_by_part"] = [[[float(np.median(lq[:, q, w, i])) for i in range(3)]
+                                                  for w in range(8) if lq[:, q, w, 0].max() > 0]
+                                                 for q in range(args.parts)]
+                out[case]["handoff_by_part"] = [[float(np.median(lq[:, q, 14, i])) for i in range(3)]
+                                                for q in range(args.parts)]
             xk = lp[:, 14, :]
             xk = xk[xk[:, 1] > 0]
             if len(xk):
@@ -187,7 +199,7 @@ def main():
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
                 for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
-                          "loop_med_per_wave", "walk_split_med(argmax,walk,compact)",
+                          "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_split_med(argmax,walk,compact)",
                           "handoff_med(misses,wait_cyc,slack_cyc)"):
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)

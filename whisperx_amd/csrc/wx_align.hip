@@ -354,12 +354,16 @@ __device__ unsigned long long wx_loop[8192 * 16 * 3];
 // ahead.  Each part then arrives at a per-segment counter;
 // the last to arrive runs the argmax, the walk and merge_repeats.
 constexpr int kMaxParts = 4;
+constexpr int kXcdStride = 8;  // blocks b and b + 8 share an XCD (MI355X: 8 XCDs, round-robin)
+__host__ __device__ constexpr unsigned split_grid(int S, int P) {
+    return (unsigned)((S + kXcdStride - 1) / kXcdStride * kXcdStride * P);
+}
 constexpr int kHaloCells = 40;  // >= HL * C = ceil(32 / C) * C for every C
 constexpr int kMaxSpin = 1 << 16;
 #ifndef WX_XSLACK
-#define WX_XSLACK 3
+#define WX_XSLACK 2
 #endif
-constexpr int kXSlack = WX_XSLACK;  // chunks a part trails its predecessor by (>= 3)
+constexpr int kXSlack = WX_XSLACK;  // chunks a part re-builds its lag to (A/B: 2 beats 3, 4)
 
 struct Split {
     int p, P;         // this part, parts per segment
@@ -435,7 +439,7 @@ struct Forward {
                                                  uint64_t (&xpre)[C], bool& lost) {
         constexpr int HL = Geometry<C, 2>::HL;
         const unsigned want = tag | (unsigned)(q & 0xFFF);
-        const uint64_t* gi = xin + (int64_t)q * xstride + l * C;
+        const uint64_t* gi = xin + (int64_t)q * xstride + min(l, HL - 1) * C;  // all lanes load
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < C; ++k) ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
@@ -445,7 +449,7 @@ struct Forward {
             ok = true;
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                if (l < HL) xpre[k] = granule_load(gi + k);
+                xpre[k] = granule_load(gi + k);
                 ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
             }
         }
@@ -550,16 +554,29 @@ struct Forward {
         bool xlost = false;  // SP: a hand-off timed out
 #pragma unroll
         for (int k = 0; k < C; ++k) xodd[k] = xeven[k] = 0;
-        if (SP && xsub && l < Geo::HL) {
+        // Prefetches are issued by every lane, unconditionally (chunk and lane clamped into the
+        // segment's granule block): a lane- or chunk-conditional load merges into the old
+        // value's register, and hipcc then waits for the load right where it is issued.
+        const int xl = min(l, Geo::HL - 1) * C;
+        if (SP && xsub) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
-                if (nch > 1) xodd[k] = granule_load(sp->xin + sp->xstride + l * C + k);
-                if (nch > 2) xeven[k] = granule_load(sp->xin + 2 * sp->xstride + l * C + k);
+                xodd[k] = granule_load(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride + xl + k);
+                xeven[k] = granule_load(sp->xin + (int64_t)min(2, nch - 1) * sp->xstride + xl + k);
             }
         }
 #ifdef WX_PHASE_TIMING
         unsigned long long acc_steps = 0, acc_bar = 0, acc_other = 0, x_miss = 0, x_wait = 0, x_slack = 0;
 #endif
+        // SP: a chunk's bitmap words are stored one chunk late, after the next hand-off wait:
+        // that wait drains vmcnt, and a store issued just before it would be waited for too.
+        unsigned wdef[C];
+#pragma unroll
+        for (int k = 0; k < C; ++k) wdef[k] = 0u;
+        auto store_deferred = [&](const int qd) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) bits[((int64_t)qd * C + k) * lanes + g] = wdef[k];
+        };
         auto chunk_iter = [&](const int q, uint64_t(&xpre)[C]) {
             WX_T(c0);
             float* buf = lds + (q % kBufs) * kChunk * VS;
@@ -610,12 +627,13 @@ struct Forward {
                 x_wait += x1 - x0;
                 x_slack += x2 - x1;
 #endif
-                if (q + 2 < nch && l < Geo::HL) {  // this set's next chunk: q + 2
+                // this set's next chunk, q + 2 (the old values are dead: keep the load below)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int k = 0; k < C; ++k)
-                        xpre[k] = granule_load(sp->xin + (int64_t)(q + 2) * sp->xstride + l * C + k);
-                }
+                for (int k = 0; k < C; ++k)
+                    xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
             }
+            if (SP && MODE == 0 && q > 0 && !halo) store_deferred(q - 1);
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
@@ -639,7 +657,11 @@ struct Forward {
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
-                    if (!halo) bits[((int64_t)q * C + k) * lanes + g] = (sh == 0) ? st.w[k] : (st.w[k] << sh);
+                    const unsigned wq = (sh == 0) ? st.w[k] : (st.w[k] << sh);
+                    if (SP)
+                        wdef[k] = wq;
+                    else if (!halo)
+                        bits[((int64_t)q * C + k) * lanes + g] = wq;
                     st.w[k] = 0u;
                 }
             }
@@ -649,6 +671,7 @@ struct Forward {
                 chunk_iter(q, xeven);
                 if (q + 1 < nch) chunk_iter(q + 1, xodd);
             }
+            if (MODE == 0 && nch > 0 && !halo) store_deferred(nch - 1);
         } else {
             for (int q = 0; q < nch; ++q) chunk_iter(q, xeven);
         }
@@ -1327,8 +1350,14 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ int tsb[3];
     __shared__ ColMapLds<VS> cml;
     const int P = SP ? a.parts : 1;
-    const int seg = SP ? (int)blockIdx.x / P : (int)blockIdx.x;
-    const int part = SP ? (int)blockIdx.x - seg * P : 0;
+    // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
+    // b % 8 — one XCD under the observed round-robin dispatch — and read its emission rows
+    // through one L2.  (Placement is a speed matter only; part p - 1 has the lower block
+    // index either way, so it starts no later than part p.)
+    const int seg = SP ? ((int)blockIdx.x / kXcdStride / P) * kXcdStride + (int)blockIdx.x % kXcdStride
+                       : (int)blockIdx.x;
+    const int part = SP ? ((int)blockIdx.x / kXcdStride) % P : 0;
+    if (SP && seg >= a.S) return;  // grid padded to a multiple of 8 segments
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     const int want = (SP || a.parts > 1) ? launch_split_bucket(d.N, a.parts, a.split_id) : bucket_id(d.N, a.mode);
     if (want != (bucket_make(C, W, H) | (SP ? kSplitFlag : 0))) return;  // another instantiation owns it
@@ -1447,7 +1476,7 @@ __global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1
     align_dp_body<C, VS, W, H>(a);
 }
 
-// Split segments: P workgroups (parts, one per CU) per segment, grid = S * P.
+// Split segments: P workgroups (parts, one per CU) per segment, grid = ceil(S / 8) * 8 * P.
 template <int C, int VS, int W>
 __global__ __launch_bounds__(kWave*(W + 1)) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
     AlignArgs a) {
@@ -2074,12 +2103,14 @@ int device_cus() {
     return cache[dev];
 }
 
-// Parts per segment of a latency launch: one CU per segment unless a split mode is asked for
-// (WX_MODE_SPLIT2..4, or WX_PARTS=2..4 for WX_MODE_AUTO / WX_MODE_LATENCY calls).  Measured on
-// config 2 (64 x T=1499): 4 parts are 3-4% faster than one CU (steps 58 vs 83 cycles, but the
-// cross-CU hand-offs add ~30 cycles per step) while every part stages all emission rows (4.4x
-// the fabric traffic), so the split is opt-in.  The CU count caps the parts: every part of
-// every segment must be resident at once.
+// Parts per segment of a latency launch.  WX_MODE_AUTO splits each segment over 4 CUs when
+// the device has 4 CUs per segment (S <= 64 on MI355X), else one CU; WX_MODE_LATENCY is one CU
+// unless WX_PARTS=2..4 asks for a split; WX_MODE_SPLIT2..4 ask explicitly.  Measured (T=1499
+// and T=2999 segments, round 1): 4 parts take 90 / 101 / 210 us for 16 x 1499 / 64 x 1499 /
+// 64 x 2999 against 107 / 110 / 309 us on one CU; 2 or 3 parts gain nothing (they pick C=2
+// buckets, whose step is as long as the one-CU bucket's).  Every part stages all emission
+// rows (4x the emission reads, ~0.5 TB/s at config 2: far from any bound).  The CU count
+// caps the parts: part p only waits for part p-1, which the dispatcher starts first.
 int split_parts(int32_t S, int mode, int32_t requested) {
     static const int forced = [] {
         const char* e = getenv("WX_PARTS");
@@ -2087,13 +2118,15 @@ int split_parts(int32_t S, int mode, int32_t requested) {
     }();
     if (mode != WX_MODE_LATENCY) return 1;
     if (requested == WX_MODE_LATENCY_1CU) return 1;
+    const int fit = device_cus() / std::max(S, 1);
     int want = 1;
     if (requested >= WX_MODE_SPLIT2 && requested <= WX_MODE_SPLIT4)
         want = requested - WX_MODE_SPLIT2 + 2;
     else if (forced)
         want = forced;
+    else if (requested == WX_MODE_AUTO && fit >= kMaxParts)
+        want = kMaxParts;
     if (want <= 1) return 1;
-    const int fit = device_cus() / std::max(S, 1);
     return std::max(1, std::min(want, fit)) >= 2 ? std::max(1, std::min(want, fit)) : 1;
 }
 
@@ -2148,7 +2181,7 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
     return fork_join(st, n, [&](int i, hipStream_t s) {
 #define WX_LAUNCH_SPLIT(CC, WW)                                                                        \
         if (ids[i] == (bucket_make(CC, WW, 1) | kSplitFlag)) {                                          \
-            const dim3 g2((unsigned)S * (unsigned)a.parts), b2(kWave * (WW + 1));                       \
+            const dim3 g2(split_grid(S, a.parts)), b2(kWave * (WW + 1));                                 \
             if (V <= 32) hipLaunchKernelGGL((align_dp_split_kernel<CC, 32, WW>), g2, b2, 0, s, a);       \
             else if (V <= 64) hipLaunchKernelGGL((align_dp_split_kernel<CC, 64, WW>), g2, b2, 0, s, a);  \
             else hipLaunchKernelGGL((align_dp_split_kernel<CC, kGatherVS, WW>), g2, b2, 0, s, a);        \
