@@ -154,6 +154,10 @@ def child(args):
             xk = xk[xk[:, 1] > 0]
             if len(xk):
                 out[case]["handoff_med(misses,wait_cyc,slack_cyc)"] = [float(np.median(xk[:, i])) for i in range(3)]
+            rk = lp[:, 13, :]
+            rk = rk[rk[:, 2] > 0]
+            if len(rk):
+                out[case]["walk_rl_med(cycles,changes,blocks)"] = [float(np.median(rk[:, i])) for i in range(3)]
             wk = lp[:, 15, :]
             wk = wk[wk[:, 1] > 0]
             if len(wk):
@@ -199,7 +203,7 @@ def main():
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
                 for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
-                          "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_split_med(argmax,walk,compact)",
+                          "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_rl_med(cycles,changes,blocks)", "walk_split_med(argmax,walk,compact)",
                           "handoff_med(misses,wait_cyc,slack_cyc)"):
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)

@@ -1005,11 +1005,13 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
 // Returns true on success (j reached 0), false where the reference returns None.
 template <int CC>
 __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bits, const Layout& lay, int b, int A) {
-    const int jj = A - lane_id();
-    if (jj < 1) return 0u;
+    // Unconditional (column clamped to 1, block to 0): the walk masks invalid lanes when it
+    // uses the word, so the load can stay in flight across blocks (a conditional load
+    // merges into its destination and hipcc then waits for it where it is issued).
+    const int jj = max(A - lane_id(), 1);
     int g, k;
     lay.locate<CC>(jj - 1, g, k);
-    return bits[((int64_t)b * lay.C + k) * lay.lanes + g];
+    return bits[((int64_t)max(b, 0) * lay.C + k) * lay.lanes + g];
 }
 
 // Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d; steps
@@ -1055,30 +1057,39 @@ __device__ __forceinline__ unsigned walk_block(unsigned win, int& d) {
 // ~N * (readlane + 8 SALU) per segment instead of T * 4 SALU + the ballot transposes.
 // Same contract as walk_block: bits of steps before the walk's start are cleared.
 __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
-    // Per change: x = word[dd] & m (m: bit positions still ahead); low = x & -x is the
-    // change; m = -(low << 1) keeps the positions after it (0 after bit 31: the loop ends
-    // and dd <= 64 is never read).  Hand-scheduled: 9 scalar-unit instructions per change
-    // (hipcc's version of the same loop took 15).
-    unsigned cm = 0u, m = 0xFFFFFFFFu, w, t;
+    // Per change: x = word[dd] & m (m: bit positions still ahead) is non-zero; p = its lowest
+    // set bit is the change; m = -2 << p keeps the positions after it (0 after bit 31: the
+    // walk leaves the block).  The chain is s_and -> s_ff1 -> s_lshl; the next lane's word
+    // (dd does not depend on the chain) is read one change ahead so v_readlane stays off
+    // it (lane dd + 1 may be past the window: read, never used).  Unrolled by four: a taken
+    // branch costs more than the rest of a change (measured ~96 cycles per change for the
+    // loop with one taken branch per change).
+    unsigned cm = 0u, m = 0xFFFFFFFFu, x, wn, t, p;
     int dd = d;
+#define WX_RL_STEP(BR)                          \
+    "s_ff1_i32_b32 %[p], %[x]\n\t"              \
+    "s_bitset1_b32 %[cm], %[p]\n\t"             \
+    "s_lshl_b32 %[m], -2, %[p]\n\t"             \
+    "s_add_u32 %[dd], %[dd], 1\n\t"             \
+    "s_add_u32 %[t], %[dd], 1\n\t"              \
+    "s_and_b32 %[x], %[wn], %[m]\n\t"           \
+    "v_readlane_b32 %[wn], %[win], %[t]\n\t" BR "\n\t"
     asm volatile(
-        "v_readlane_b32 %[w], %[win], %[dd]\n\t"
-        "s_and_b32 %[w], %[w], %[m]\n\t"
+        "v_readlane_b32 %[x], %[win], %[dd]\n\t"
+        "s_add_u32 %[t], %[dd], 1\n\t"
+        "v_readlane_b32 %[wn], %[win], %[t]\n\t"
+        "s_and_b32 %[x], %[x], %[m]\n\t"
         "s_cbranch_scc0 2f\n"
         "1:\n\t"
-        "s_sub_u32 %[t], 0, %[w]\n\t"
-        "s_and_b32 %[w], %[w], %[t]\n\t"
-        "s_or_b32 %[cm], %[cm], %[w]\n\t"
-        "s_lshl_b32 %[w], %[w], 1\n\t"
-        "s_sub_u32 %[m], 0, %[w]\n\t"
-        "s_add_u32 %[dd], %[dd], 1\n\t"
-        "v_readlane_b32 %[w], %[win], %[dd]\n\t"
-        "s_and_b32 %[w], %[w], %[m]\n\t"
-        "s_cbranch_scc1 1b\n"
+        WX_RL_STEP("s_cbranch_scc0 2f")
+        WX_RL_STEP("s_cbranch_scc0 2f")
+        WX_RL_STEP("s_cbranch_scc0 2f")
+        WX_RL_STEP("s_cbranch_scc1 1b")
         "2:"
-        : [dd] "+s"(dd), [cm] "+s"(cm), [m] "+s"(m), [w] "=&s"(w), [t] "=&s"(t)
+        : [dd] "+s"(dd), [cm] "+s"(cm), [m] "+s"(m), [x] "=&s"(x), [wn] "=&s"(wn), [t] "=&s"(t), [p] "=&s"(p)
         : [win] "v"(win)
         : "scc");
+#undef WX_RL_STEP
     d = dd;
     return cm;
 }
@@ -1089,44 +1100,117 @@ __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
 // without an early-exit test.  Per block only the change mask is kept (cmask[b]);
 // start frames are compacted from it afterwards.  Returns the lowest block touched, or -1
 // where the reference returns None.
-template <class LoadWin>  // LoadWin(b, A): this lane's word of window column A - lane in block b
-__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask) {
+//
+// The bitmap words are global loads (written by other waves or CUs), so the walk keeps three
+// blocks' windows in flight: the window of block b - 3 is issued when block b starts, at the
+// column A the walk has then; lane i loads the words of columns A - i and A - 64 - i.  The
+// path moves at most 32 columns per block, so block b - 3 starts at most 64 columns left of
+// A and ends within 128 of it.  At use, the 64 lanes from the walk's offset are gathered
+// into one word per lane (two ds_bpermutes, skipped while the block fits the first word).
+template <class LoadWin>  // LoadWin(b, A): this lane's word of column A - lane in block b (clamped)
+__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask, bool cmask_in_lds) {
     if (t_start <= 0 || N <= 0) return -1;
-    int j = N;
-    int b = (t_start - 1) >> 5;
-    int A = j;
-    const int s_hi = (t_start - 1) & 31;  // steps above t_start-1 do not exist: clear their bits
-    unsigned win = load_win(b, A) & (0xFFFFFFFFu << (31 - s_hi));
-    int An = A;
-    unsigned nxt = (b > 0) ? load_win(b - 1, An) : 0u;
-    int d = 0;
-#ifdef WX_WALK_BALLOT
-    unsigned cm = walk_block(win, d);
+    struct Win {
+        unsigned lo, hi;
+        int A;
+    };
+    const int lane = lane_id();
+    int b = uniform((t_start - 1) >> 5);
+    int j = uniform(N);
+    unsigned first_mask = 0xFFFFFFFFu << (31 - ((t_start - 1) & 31));  // steps above t_start - 1
+#ifdef WX_PHASE_TIMING
+    unsigned long long t_rl = 0, n_ch = 0, n_bl = 0;
+    auto dump = [&]() {
+        if (lane == 0 && blockIdx.x < 8192) {
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + 13) * 3;
+            o[0] = t_rl;
+            o[1] = n_ch;
+            o[2] = n_bl;
+        }
+    };
 #else
-    unsigned cm = walk_block_rl(win, d);
+    auto dump = [] {};
 #endif
-    while (true) {
-        cmask[b] = cm;
-        j = uniform(A - d);
-        if (j <= 0) return b;
-        if (b == 0) return -1;
+    unsigned cmv = 0u;    // change masks of blocks gb + lane
+    int gtop = b & 63;    // highest lane of the current group the walk has written
+    auto issue = [&](Win& w, int bb, int A) {
+        w.A = uniform(A);
+        w.lo = load_win(bb, A);
+        w.hi = load_win(bb, A - 64);
+    };
+    // walks block b with window w; false when the walk is over (result in res)
+    auto block = [&](Win& w, int& res) -> bool {
+        const int d = uniform(w.A - j);  // 0 .. 96
+        unsigned win;
+        int dd;
+        if (d <= 31) {
+            win = (w.A - lane >= 1) ? w.lo : 0u;
+            dd = d;
+        } else {
+            const int o = d + lane;  // column w.A - o
+            const unsigned a = (unsigned)__shfl((int)w.lo, o & 63);
+            const unsigned h = (unsigned)__shfl((int)w.hi, o & 63);
+            win = (w.A - o >= 1 && o < 128) ? (o < 64 ? a : h) : 0u;
+            dd = 0;
+        }
+        win &= first_mask;
+        first_mask = 0xFFFFFFFFu;
+        const int d0 = dd;
+#ifdef WX_WALK_BALLOT
+        const unsigned cm = walk_block(win, dd);
+#else
+#ifdef WX_PHASE_TIMING
+        WX_T(rl0);
+#endif
+        const unsigned cm = walk_block_rl(win, dd);
+#ifdef WX_PHASE_TIMING
+        WX_T(rl1);
+        t_rl += rl1 - rl0;
+        n_ch += __popc(cm);
+        ++n_bl;
+#endif
+#endif
+        // change masks are collected in lane b % 64 and stored 64 blocks at a time, through
+        // an explicit LDS or global store (a flat store in the loop makes hipcc drain every
+        // pending load at each wait)
+        cmv = lane == (b & 63) ? cm : cmv;
+        j = uniform(j - (dd - d0));
+        const bool done = j <= 0 || b == 0;
+        if (done || (b & 63) == 0) {
+            const int gb = b & ~63;
+            if (lane >= (b & 63) && lane <= gtop) {
+                if (cmask_in_lds)
+                    ((__attribute__((address_space(3))) unsigned*)cmask)[gb + lane] = cmv;
+                else
+                    ((__attribute__((address_space(1))) unsigned*)cmask)[gb + lane] = cmv;
+            }
+            gtop = 63;
+        }
+        issue(w, b - 3, j);  // unconditional (a conditional refill would merge and wait)
+        if (done) {
+            res = j <= 0 ? b : -1;
+            dump();
+            return false;
+        }
         --b;
-        win = nxt;
-        A = An;
-        An = j;
-        nxt = (b > 0) ? load_win(b - 1, An) : 0u;
-        d = A - j;
-#ifdef WX_WALK_BALLOT
-        cm = walk_block(win, d);
-#else
-        cm = walk_block_rl(win, d);
-#endif
+        return true;
+    };
+    Win w0, w1, w2;
+    issue(w0, b, N);
+    issue(w1, b - 1, N);
+    issue(w2, b - 2, N);
+    int res = -1;
+    for (;;) {
+        if (!block(w0, res)) return res;
+        if (!block(w1, res)) return res;
+        if (!block(w2, res)) return res;
     }
 }
 
 template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
-__device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask) {
-    return walk_impl([&](int b, int A) { return load_window<CC>(bits, lay, b, A); }, N, t_start, cmask);
+__device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
+                    bool cmask_in_lds) {
+    return walk_impl([&](int b, int A) { return load_window<CC>(bits, lay, b, A); }, N, t_start, cmask, cmask_in_lds);
 }
 
 // start[k] = k-th change frame in increasing time: a popcount prefix over the change masks
@@ -1437,7 +1521,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
             tsb[0] = ts;
         }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W * P), d.N, ts, cmask);
+        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W * P), d.N, ts, cmask, d.T <= kMaxLdsFrames);
 #ifdef WX_PHASE_TIMING
         WX_T(w2);
 #endif
@@ -1641,7 +1725,7 @@ __global__ __launch_bounds__(256) void backtrack_kernel(BacktrackArgs a) {
         lay.n_short = 0;
         lay.lanes = kWave;
         unsigned* cmask = a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk<0>(bits, lay, N, ts, cmask);
+        const int b_lo = walk<0>(bits, lay, N, ts, cmask, false);
         if (b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
