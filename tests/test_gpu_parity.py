@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 # throughput; latency (auto parts); latency on one CU; split over 2 / 3 / 4 CUs
-MODES = [0, 1, 2, 12, 13, 14]
+MODES = [-1, 0, 1, 2, 12, 13, 14]  # -1: WX_MODE_AUTO (small batches: split over 4 CUs)
 
 
 @pytest.fixture(scope="module", autouse=True)
