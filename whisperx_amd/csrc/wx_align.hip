@@ -361,9 +361,9 @@ __host__ __device__ constexpr unsigned split_grid(int S, int P) {
 constexpr int kHaloCells = 40;  // >= HL * C = ceil(32 / C) * C for every C
 constexpr int kMaxSpin = 1 << 16;
 #ifndef WX_XSLACK
-#define WX_XSLACK 2
+#define WX_XSLACK 1
 #endif
-constexpr int kXSlack = WX_XSLACK;  // chunks a part re-builds its lag to (A/B: 2 beats 3, 4)
+constexpr int kXSlack = WX_XSLACK;  // chunks a part re-builds its lag to (A/B: 1 >= 2 > 3 > 4)
 
 struct Split {
     int p, P;         // this part, parts per segment
