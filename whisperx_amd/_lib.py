@@ -179,6 +179,37 @@ class Batch:
         self.min_N = min(self.Ns) if self.Ns else 0
         self.max_N = max(self.Ns) if self.Ns else 0
 
+    @classmethod
+    def from_csr(cls, em: torch.Tensor, Ts, tokens, blank_ids):
+        """A batch over an already packed [sum_T, V] fp32 device matrix (segment s owns rows
+        sum(Ts[:s]) .. +Ts[s]), e.g. the one _emissions_csr writes log_softmax into."""
+        self = cls.__new__(cls)
+        if len(Ts) != len(tokens) or len(tokens) != len(blank_ids):
+            raise ValueError("Ts, tokens and blank_ids must have the same length")
+        if em.dim() != 2 or em.dtype != torch.float32 or not em.is_contiguous() or em.shape[0] != sum(Ts):
+            raise ValueError("em must be a contiguous [sum(Ts), V] float32 tensor")
+        self.S = len(Ts)
+        self.device = em.device
+        self.V = int(em.shape[1])
+        self.Ts = [int(t) for t in Ts]
+        self.Ns = [len(t) for t in tokens]
+        self.em_off = [0]
+        for T in self.Ts:
+            self.em_off.append(self.em_off[-1] + T)
+        self.tok_off = [0]
+        for N in self.Ns:
+            self.tok_off.append(self.tok_off[-1] + N)
+        self.sum_T = self.em_off[-1]
+        self.em = em
+        flat = [int(x) for t in tokens for x in t]
+        self.tok = _h2d(flat if flat else [0], torch.int32, self.device)
+        self.blank = _h2d([int(b) for b in blank_ids] or [0], torch.int32, self.device)
+        self.em_off_d = _dev_i64(self.em_off, self.device)
+        self.tok_off_d = _dev_i64(self.tok_off, self.device)
+        self.min_N = min(self.Ns) if self.Ns else 0
+        self.max_N = max(self.Ns) if self.Ns else 0
+        return self
+
 
 def _validate(b: Batch):
     if b.V < 1 or b.V > MAX_VOCAB:

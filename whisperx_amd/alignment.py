@@ -26,13 +26,15 @@ There is no CPU fallback: without a HIP device the DP raises.
 from __future__ import annotations
 
 import math
+import os
+import time
 from dataclasses import dataclass
 from typing import Callable, Iterable, List, Optional, Union
 
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, emission
 from .audio import SAMPLE_RATE, load_audio
 from .types import AlignedTranscriptionResult, SingleAlignedSegment, SingleSegment, SingleWordSegment
 from .utils import interpolate_nans
@@ -164,6 +166,29 @@ def _sentence_spans(text: str):
 
 
 # ------------------------------------------------------------------------------- align()
+# WX_PROFILE=1: synchronise at align()'s phase boundaries and accumulate wall time per phase
+# in PHASE_TIMES (diagnostics only; the sync points remove the overlap of the phases)
+_PROFILE = bool(os.environ.get("WX_PROFILE"))
+PHASE_TIMES: dict = {}
+
+
+class _Phase:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if _PROFILE:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self.t0 = time.perf_counter()
+
+    def __exit__(self, *exc):
+        if _PROFILE:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            PHASE_TIMES[self.name] = PHASE_TIMES.get(self.name, 0.0) + time.perf_counter() - self.t0
+
+
 def _prepare(segment: dict, dictionary, lang: str):
     """alignment.py:137-177: clean chars/indices, clean words, sentence spans (mutates)."""
     text = segment["text"]
@@ -187,8 +212,8 @@ def _prepare(segment: dict, dictionary, lang: str):
     segment["sentence_spans"] = _sentence_spans(text)
 
 
-def _emission(model, model_type, waveform_segment, device):
-    """alignment.py:217-233 on the device; returns the [T, V] log-probabilities (on device)."""
+def _logits(model, model_type, waveform_segment, device):
+    """alignment.py:217-232 on the device: the [1, T, V] logits of one unpadded forward."""
     if waveform_segment.shape[-1] < 400:
         lengths = torch.as_tensor([waveform_segment.shape[-1]]).to(device)
         waveform_segment = torch.nn.functional.pad(waveform_segment, (0, 400 - waveform_segment.shape[-1]))
@@ -201,38 +226,91 @@ def _emission(model, model_type, waveform_segment, device):
             emissions = model(waveform_segment.to(device)).logits
         else:
             raise NotImplementedError(f"Align model of type {model_type} not supported.")
-        emissions = torch.log_softmax(emissions, dim=-1)
-    return emissions[0].detach()
+    return emissions
+
+
+def _emission(model, model_type, waveform_segment, device):
+    """alignment.py:217-235 without the host copy: the [T, V] log-probabilities (on device)."""
+    with torch.inference_mode():
+        return torch.log_softmax(_logits(model, model_type, waveform_segment, device), dim=-1)[0].detach()
+
+
+class _EmissionsCSR:
+    """Log-probabilities of S segments packed as one [sum_T, V] fp32 device matrix (the DP
+    kernel's input layout); iterating yields each segment's [T, V] row slice."""
+
+    def __init__(self, em: torch.Tensor, Ts):
+        self.em = em
+        self.Ts = list(Ts)
+        self.off = [0]
+        for T in self.Ts:
+            self.off.append(self.off[-1] + T)
+
+    def __len__(self):
+        return len(self.Ts)
+
+    def __getitem__(self, i):
+        return self.em[self.off[i]: self.off[i + 1]]
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
+def _vocab_size(model, model_type):
+    if model_type == "huggingface":
+        head = getattr(model, "lm_head", None)
+    else:
+        head = getattr(model, "aux", None)
+    n = getattr(head, "out_features", None)
+    return int(n) if n else None
 
 
 _EMISSION_STREAMS = {}
 
 
 def _emissions(model, model_type, waveforms, device, n_streams: int = 4):
-    """_emission for every segment, one unpadded forward each (padding would change
-    wav2vec2's logits), issued round-robin on `n_streams` HIP streams: one 30 s forward's
-    GEMMs (1,499 rows) fill a fraction of the GPU, so consecutive segments overlap.  Same
-    kernels per segment as one-at-a-time; joined back onto the current stream."""
+    """Emissions of every segment, one unpadded forward each (padding would change wav2vec2's
+    logits, alignment.py:217-233), issued round-robin on `n_streams` HIP streams: one 30 s
+    forward's GEMMs (1,499 rows) fill a fraction of the GPU, so consecutive segments overlap.
+    On a HIP device each forward's log_softmax writes straight into its rows of one packed
+    [sum_T, V] matrix (returned as _EmissionsCSR), which the DP reads in place; the model's
+    convolutions take the length-agnostic GEMM route (emission.prepare_model) unless
+    WX_MIOPEN_CONV=1.  Joined back onto the current stream."""
     dev = torch.device(device) if not isinstance(device, torch.device) else device
-    if dev.type != "cuda" or n_streams <= 1 or len(waveforms) <= 1:
+    if dev.type != "cuda":
         return [_emission(model, model_type, w, device) for w in waveforms]
+    if not os.environ.get("WX_MIOPEN_CONV"):
+        emission.prepare_model(model)
+    V = _vocab_size(model, model_type)
+    cfg_model = model if model_type == "huggingface" else None
+    Ts = [emission.n_frames(int(w.shape[-1]), cfg_model) for w in waveforms]
+    main = torch.cuda.current_stream(dev)
+    if V is None or not waveforms:
+        return [_emission(model, model_type, w, device) for w in waveforms]
+    csr = _EmissionsCSR(torch.empty((max(sum(Ts), 1), V), dtype=torch.float32, device=dev), Ts)
+    if sum(Ts) == 0:
+        csr.em = csr.em[:0]
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), n_streams)
     streams = _EMISSION_STREAMS.get(key)
     if streams is None:
-        streams = [torch.cuda.Stream(device=dev) for _ in range(n_streams)]
+        streams = [torch.cuda.Stream(device=dev) for _ in range(max(n_streams, 1))]
         _EMISSION_STREAMS[key] = streams
-    main = torch.cuda.current_stream(dev)
-    out = []
+    bad = False
     for i, w in enumerate(waveforms):
-        st = streams[i % n_streams]
+        st = streams[i % len(streams)]
         st.wait_stream(main)
         with torch.cuda.stream(st):
-            em = _emission(model, model_type, w, device)
-        em.record_stream(main)
-        out.append(em)
+            lg = _logits(model, model_type, w, device)
+            if tuple(lg.shape) != (1, Ts[i], V):
+                bad = True  # the model's frame geometry is not wav2vec2's: fall back below
+                break
+            with torch.inference_mode():
+                emission.log_softmax_into(lg[0], csr[i])
     for st in streams:
         main.wait_stream(st)
-    return out
+    if bad:
+        return [_emission(model, model_type, w, device) for w in waveforms]
+    return csr
 
 
 def _dp_device(device):
@@ -281,12 +359,13 @@ def align(
 
     # 1. text preparation (mutates the input segments like the reference)
     total_segments = len(transcript)
-    for sdx, segment in enumerate(transcript):
-        if print_progress:
-            base_progress = ((sdx + 1) / total_segments) * 100
-            percent_complete = (50 + base_progress / 2) if combined_progress else base_progress
-            print(f"Progress: {percent_complete:.2f}%...")
-        _prepare(segment, model_dictionary, model_lang)
+    with _Phase("prepare"):
+        for sdx, segment in enumerate(transcript):
+            if print_progress:
+                base_progress = ((sdx + 1) / total_segments) * 100
+                percent_complete = (50 + base_progress / 2) if combined_progress else base_progress
+                print(f"Progress: {percent_complete:.2f}%...")
+            _prepare(segment, model_dictionary, model_lang)
 
     # 2a. emissions for every alignable segment, queued on the device
     blank_id = blank_id_of(model_dictionary)
@@ -311,12 +390,24 @@ def align(
         toks.append(tokens)
         blanks.append(blank_id)
         meta.append((text_clean, waveform_segment.size(0)))
-    ems = _emissions(model, model_type, ems, device)
+    with _Phase("emission"):
+        ems = _emissions(model, model_type, ems, device)
 
     # 2b. one fused DP launch for all segments
-    results = _run_dp(ems, toks, blanks, dp_dev) if ems else []
+    with _Phase("dp"):
+        results = _run_dp(ems, toks, blanks, dp_dev) if len(ems) else []
 
     # 2c. timestamps and aggregation, in segment order (same prints, same order)
+    with _Phase("aggregate"):
+        aligned_segments = _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method,
+                                          return_char_alignments)
+    word_segments: List[SingleWordSegment] = []
+    for segment in aligned_segments:
+        word_segments += segment["words"]
+    return {"segments": aligned_segments, "word_segments": word_segments}
+
+
+def _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method, return_char_alignments):
     aligned_segments: List[SingleAlignedSegment] = []
     for sdx, segment in enumerate(transcript):
         t1, t2, text = segment["start"], segment["end"], segment["text"]
@@ -340,15 +431,14 @@ def align(
         _, n_channels = meta[bi]
         aligned_segments += aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang,
                                               interpolate_method, return_char_alignments)
-
-    word_segments: List[SingleWordSegment] = []
-    for segment in aligned_segments:
-        word_segments += segment["words"]
-    return {"segments": aligned_segments, "word_segments": word_segments}
+    return aligned_segments
 
 
 def _run_dp(ems, toks, blanks, dev):
-    batch = _lib.Batch(ems, toks, blanks, device=dev)
+    if isinstance(ems, _EmissionsCSR) and ems.em.device == dev:
+        batch = _lib.Batch.from_csr(ems.em, ems.Ts, toks, blanks)
+    else:
+        batch = _lib.Batch(list(ems), toks, blanks, device=dev)
     seg_start, seg_end, seg_score, t_start, status = _lib.align_dp(batch)
     # one device->host copy of everything the host needs
     ss = seg_start.cpu().numpy()
