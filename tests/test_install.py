@@ -1,0 +1,100 @@
+"""The drop-in boundary, proven on the reference package itself (build container only):
+import /root/reference/whisperx behind stand-ins for the modules this image lacks (SURVEY.md
+§8(c) recipe, plus ctranslate2 / faster_whisper for asr.py), apply whisperx_amd.install(),
+and check that every call site the CLI and the ASR pipeline use now resolves to
+whisperx_amd's functions (transcribe.py:9,188,201,203; asr.py:13,187; __init__.py:2).
+
+Runs in a subprocess: the stand-ins must not leak into the other tests' sys.modules."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent(r'''
+    import sys, types
+    from importlib.machinery import ModuleSpec
+    from types import SimpleNamespace
+    import transformers, torch  # transformers before the torchaudio stand-in
+
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        m.__spec__ = ModuleSpec(name, None)
+        for k, v in attrs.items():
+            setattr(m, k, v)
+        sys.modules[name] = m
+        return m
+
+    mod("torchaudio", pipelines=SimpleNamespace(__all__=[]))
+    class PunktParameters:
+        def __init__(self): self.abbrev_types = set()
+    class PunktSentenceTokenizer:
+        def __init__(self, params=None): pass
+        def span_tokenize(self, text): yield (0, len(text.rstrip()))
+    punkt = mod("nltk.tokenize.punkt", PunktParameters=PunktParameters, PunktSentenceTokenizer=PunktSentenceTokenizer)
+    mod("nltk.tokenize", punkt=punkt); mod("nltk")
+    mod("pyannote"); mod("pyannote.audio", Model=object, Pipeline=object); mod("pyannote.audio.core")
+    mod("pyannote.audio.core.io", AudioFile=object)
+    mod("pyannote.audio.pipelines", VoiceActivityDetection=object)
+    mod("pyannote.audio.pipelines.utils", PipelineModel=object)
+    mod("pyannote.core", Annotation=object, Segment=object, SlidingWindowFeature=object, SlidingWindow=object)
+    mod("ctranslate2", StorageView=object)
+    fw_tok = mod("faster_whisper.tokenizer", Tokenizer=object)
+    fw_tr = mod("faster_whisper.transcribe", TranscriptionOptions=object, get_ctranslate2_storage=None)
+    mod("faster_whisper", WhisperModel=object, tokenizer=fw_tok, transcribe=fw_tr)
+
+    sys.path.insert(0, sys.argv[1])   # /root/reference
+    sys.path.insert(0, sys.argv[2])   # this repo
+    import whisperx
+    import whisperx.transcribe, whisperx.asr, whisperx.alignment, whisperx.vad, whisperx.utils
+    ref_align = whisperx.transcribe.align
+    assert ref_align is whisperx.alignment.align          # before: the reference CPU path
+
+    import whisperx_amd
+    from whisperx_amd import vad as amd_vad, writers as amd_writers
+    rebound = whisperx_amd.install(whisperx)
+    assert whisperx_amd.integration.installed(whisperx)
+
+    # module attributes
+    assert whisperx.align is whisperx_amd.align and whisperx.load_align_model is whisperx_amd.load_align_model
+    assert whisperx.transcribe.align is whisperx_amd.align
+    assert whisperx.transcribe.load_align_model is whisperx_amd.load_align_model
+    assert whisperx.transcribe.get_writer is amd_writers.get_writer
+    assert whisperx.alignment.align is whisperx_amd.align
+    assert whisperx.alignment.get_trellis is whisperx_amd.get_trellis
+    assert whisperx.asr.merge_chunks is amd_vad.merge_chunks
+    assert whisperx.vad.merge_chunks is amd_vad.merge_chunks
+    # what the call sites resolve at call time (module globals of the calling functions)
+    assert whisperx.transcribe.cli.__globals__["align"] is whisperx_amd.align
+    assert whisperx.transcribe.cli.__globals__["load_align_model"] is whisperx_amd.load_align_model
+    assert whisperx.asr.FasterWhisperPipeline.transcribe.__globals__["merge_chunks"] is amd_vad.merge_chunks
+    print("rebound", len(rebound))
+''')
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "whisperx")), reason="reference tree absent (GPU box)")
+def test_install_rebinds_reference_call_sites():
+    r = subprocess.run([sys.executable, "-c", SCRIPT, REF, ROOT], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rebound" in r.stdout
+
+
+def test_install_on_a_package_without_reference_modules():
+    import types
+
+    import whisperx_amd
+
+    pkg = types.ModuleType("fake_whisperx_pkg")
+    pkg.align = None
+    sys.modules["fake_whisperx_pkg"] = pkg
+    try:
+        done = whisperx_amd.install(pkg, import_missing=False)
+        assert done == [("fake_whisperx_pkg", "align")]
+        assert pkg.align is whisperx_amd.align
+    finally:
+        del sys.modules["fake_whisperx_pkg"]

@@ -28,5 +28,6 @@ from .alignment import (  # noqa: F401
 from .audio import SAMPLE_RATE, load_audio  # noqa: F401
 from .vad import Binarize, merge_chunks  # noqa: F401
 from .writers import get_writer, format_timestamp  # noqa: F401
+from .integration import install  # noqa: F401
 
 __version__ = "0.1.0"
