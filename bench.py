@@ -32,8 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-W2V_VOCAB = ["<pad>", "<s>", "</s>", "<unk>", "|", "E", "T", "A", "O", "N", "I", "H", "S", "R",
-             "D", "L", "U", "M", "W", "C", "F", "G", "Y", "P", "B", "V", "K", "'", "X", "J", "Q", "Z"]
+from whisperx_amd.synthetic import W2V_VOCAB  # noqa: E402  (no GPU touched at import)
 FRAME_S = 0.02  # wav2vec2 frame hop (320 samples at 16 kHz)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
@@ -238,6 +237,198 @@ def e2e_config3(device, seed=3):
                     "synthetic scores/audio/transcripts"}
 
 
+def _w2v_base(device, seed):
+    """Random-weight wav2vec2-base (WAV2VEC2_ASR_BASE_960H's architecture, V=32): there are
+    no checkpoints offline, and the forward's cost does not depend on the weights."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    torch.manual_seed(seed)
+    return Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).to(device).eval()
+
+
+def corpus_config4(device, rank, world, dist_on, seed=4):
+    """BASELINE config 4: a 10 h corpus of 40 files (log-uniform 1-60 min), sharded over the
+    ranks longest-first (distributed.shard_files); per file, as transcribe.py:172-205 runs it
+    one file after another: VAD scores -> merge_chunks (GPU Binarize, 30 s chunks,
+    asr.py:187) -> segments rounded to 3 dp (asr.py:226-232) -> align() with the random-weight
+    wav2vec2-base forward per chunk and the fused DP.  Inputs (scores, audio, transcripts) are
+    synthetic and resident before the clock starts; the clock covers merge_chunks + align()
+    for every file of every rank (barrier, max over ranks)."""
+    import whisperx_amd
+    from whisperx_amd import synthetic
+    from whisperx_amd.distributed import shard_files
+    from whisperx_amd.vad import merge_chunks
+
+    durs = synthetic.corpus_durations(seed)
+    mine = shard_files(durs, world)[rank]
+    model = _w2v_base(device, seed)
+    meta = {"language": "en", "dictionary": synthetic.w2v_dictionary(), "type": "huggingface"}
+    longest = max([durs[i] for i in mine], default=30.0)
+    g = torch.Generator().manual_seed(seed)
+    audio_buf = torch.randn(int(longest * 16000) + 16000, generator=g) * 0.1
+    files = [(i, synthetic.vad_scores(seed * 1000 + i, durs[i]), audio_buf[: int(durs[i] * 16000)]) for i in mine]
+    tr = synthetic.Transcriber(seed + rank)
+    # warm-up outside the clock (kernels, GEMM heuristics, streams)
+    whisperx_amd.align(tr.segments([{"start": 0.0, "end": 30.0}, {"start": 30.0, "end": 47.3}]), model, meta,
+                       audio_buf[: 60 * 16000], device)
+    merge_chunks(synthetic.vad_scores(1, 60.0), 30, 0.5, 0.363)
+    torch.cuda.synchronize()
+    if dist_on:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    n_seg, n_words = 0, 0
+    for i, scores, audio in files:
+        chunks = merge_chunks(scores, 30, 0.5, 0.363)
+        segs = tr.segments(chunks)
+        out = whisperx_amd.align(segs, model, meta, audio, device)
+        n_seg += len(segs)
+        n_words += len(out["word_segments"])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist_on:
+        torch.distributed.barrier()
+        el_max = _allreduce([el], "max")[0]
+        n_seg_all, n_words_all, n_files = _allreduce([n_seg, n_words, len(mine)], "sum")
+    else:
+        el_max, n_seg_all, n_words_all, n_files = el, n_seg, n_words, len(mine)
+    total = float(sum(durs))
+    return {"files": int(n_files), "audio_sec": total, "n_gpus": world, "segments": int(n_seg_all),
+            "words": int(n_words_all), "wall_s": el_max, "audio_sec_per_s": total / el_max,
+            "segments_per_s": n_seg_all / el_max, "scaling": "strong (fixed 10 h corpus)",
+            "shard": "LPT by duration (distributed.shard_files)",
+            "note": "per file: GPU merge_chunks(30 s) + align() incl. random-weight wav2vec2-base fp32 "
+                    "forward per chunk; synthetic VAD scores/audio/transcripts resident before the clock"}
+
+
+def _cpu_reference_align(segs, model_cpu, dictionary, audio):
+    """The reference's CPU align() path (device='cpu'): CPU forward + log_softmax per segment
+    (alignment.py:209-235), the DP on the CPU (oracle TorchPort: get_trellis / backtrack /
+    merge_repeats with the reference's per-timestep torch ops, :359-454), then the host
+    timestamps/aggregation (whisperx_amd.alignment.aggregate_segment: the pandas-free
+    restatement of :252-347, faster than the reference's pandas, so the baseline is
+    conservative).  Returns (result dicts, seconds per phase)."""
+    from oracle.oracle import TorchPort
+    from whisperx_amd import alignment as A
+
+    port = TorchPort()
+    t_fwd = t_dp = t_agg = 0.0
+    out = []
+    for seg in segs:
+        seg = dict(seg)
+        A._prepare(seg, dictionary, "en")
+        tokens = [dictionary[c] for c in "".join(seg["clean_char"])]
+        wav = audio[:, int(seg["start"] * 16000): int(seg["end"] * 16000)]
+        t0 = time.perf_counter()
+        with torch.inference_mode():
+            em = torch.log_softmax(model_cpu(wav).logits, -1)[0]
+        t1 = time.perf_counter()
+        merged = port.align_dp(em, tokens, 0)
+        t2 = time.perf_counter()
+        if merged is not None:
+            ss = np.array([m[1] for m in merged])
+            se = np.array([m[2] for m in merged])
+            sc = np.array([m[3] for m in merged])
+            out += A.aggregate_segment(seg, ss, se, sc, em.shape[0], 1, "en", "nearest", False)
+        t3 = time.perf_counter()
+        t_fwd, t_dp, t_agg = t_fwd + t1 - t0, t_dp + t2 - t1, t_agg + t3 - t2
+    return out, (t_fwd, t_dp, t_agg)
+
+
+def _e2e_inputs(n_seg, seed):
+    from whisperx_amd import synthetic
+
+    tr = synthetic.Transcriber(seed)
+    segs = tr.segments([{"start": 30.0 * k, "end": 30.0 * (k + 1)} for k in range(n_seg)])
+    g = torch.Generator().manual_seed(seed)
+    audio = torch.randn(30 * n_seg * 16000, generator=g) * 0.1
+    return segs, audio
+
+
+def cpu_align_baseline(threads, budget_s=20.0, seed=11):
+    """BASELINE config 1 on the host CPU: one 30 s EN clip through the reference-structured
+    CPU align() (random-weight wav2vec2-base forward, T=1499, ~70 words), at `threads` torch
+    threads, repeated until `budget_s`."""
+    from whisperx_amd import synthetic
+
+    old = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        model = _w2v_base("cpu", seed)
+        segs, audio = _e2e_inputs(1, seed)
+        audio = audio[None]
+        _cpu_reference_align(segs, model, synthetic.w2v_dictionary(), audio)  # warm-up
+        n, tot = 0, [0.0, 0.0, 0.0]
+        while sum(tot) < budget_s and n < 50:
+            _, ph = _cpu_reference_align(segs, model, synthetic.w2v_dictionary(), audio)
+            tot = [a + b for a, b in zip(tot, ph)]
+            n += 1
+    finally:
+        torch.set_num_threads(old)
+    el = sum(tot)
+    return {"value": 30.0 * n / el, "unit": "audio-sec/s", "threads": threads, "clips": n,
+            "ms_per_clip": 1000 * el / n, "forward_ms": 1000 * tot[0] / n, "dp_ms": 1000 * tot[1] / n,
+            "aggregate_ms": 1000 * tot[2] / n}
+
+
+def mae_e2e(device, n_seg=4, seed=7):
+    """north_star parity on the real emission path: the same random-weight wav2vec2-base and
+    the same audio through (a) align() on the GPU (GPU forward + fused HIP DP) and (b) the
+    reference's CPU path (CPU forward + CPU DP).  Word start/end MAE in ms and the number of
+    segments whose char token paths differ."""
+    import whisperx_amd
+    from whisperx_amd import synthetic
+
+    model = _w2v_base(device, seed)
+    model_cpu = _w2v_base("cpu", seed)
+    segs, audio = _e2e_inputs(n_seg, seed)
+    dictionary = synthetic.w2v_dictionary()
+    meta = {"language": "en", "dictionary": dictionary, "type": "huggingface"}
+    gpu = whisperx_amd.align([dict(s) for s in segs], model, meta, audio, device)["segments"]
+    cpu, _ = _cpu_reference_align(segs, model_cpu, dictionary, audio[None])
+    errs, n_words, n_diff = [], 0, 0
+    for a, b in zip(gpu, cpu):
+        wa, wb = a["words"], b["words"]
+        seg_diff = False
+        for x, y in zip(wa, wb):
+            for k in ("start", "end"):
+                if k in x and k in y:
+                    errs.append(abs(x[k] - y[k]) * 1000.0)
+                    seg_diff |= x[k] != y[k]
+            n_words += 1
+        n_diff += int(seg_diff or len(wa) != len(wb))
+    return {"mae_ms": float(np.mean(errs)) if errs else None, "max_ms": float(np.max(errs)) if errs else None,
+            "words": n_words, "segments": len(gpu), "segments_with_differing_times": n_diff,
+            "frame_ms": 20.0, "vs": "reference CPU align() path (CPU forward + CPU DP), same weights and audio"}
+
+
+def _allreduce(vals, op):
+    """All-reduce a few host numbers (fp64) over the process group: on the rank's GPU for
+    RCCL, on the CPU for gloo."""
+    t = torch.tensor(vals, dtype=torch.float64, device=_allreduce.dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX if op == "max" else torch.distributed.ReduceOp.SUM)
+    return [float(x) for x in t.cpu().tolist()]
+
+
+_allreduce.dev = torch.device("cpu")
+
+
+def _spawn_ranks(args):
+    """--gpus N > 1 without a torchrun environment: launch N ranks as a child torchrun and
+    exit with its status.  The parent never touches the GPU (no HIP init before the child)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,23 +438,37 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-scale", action="store_true")
+    ap.add_argument("--no-corpus", action="store_true", help="skip the config-4 10 h corpus leg")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one GPU per rank (LOCAL_RANK); WX_DIST_BACKEND=gloo rehearses the multi-rank path on a
+    # box with fewer GPUs than ranks (ranks then share GPUs; RCCL refuses that)
+    backend = os.environ.get("WX_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    gpu = local_rank % n_dev if (backend == "gloo" and n_dev) else local_rank
+    torch.cuda.set_device(gpu)
+    device = torch.device("cuda", gpu)
     if dist_on:
-        torch.distributed.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=device)
+        else:
+            torch.distributed.init_process_group(backend)
+    _allreduce.dev = device if backend == "nccl" else torch.device("cpu")
 
     from whisperx_amd import _lib
     from whisperx_amd.distributed import broadcast_dictionary
 
     _lib.load()
     dictionary = {c.lower(): i for i, c in enumerate(W2V_VOCAB)} if rank == 0 else None
-    dictionary = broadcast_dictionary(dictionary, device) if dist_on else dictionary
+    dictionary = broadcast_dictionary(dictionary, _allreduce.dev if backend != "nccl" else device) if dist_on else dictionary
     V = len(dictionary)
 
     # ---- the config-2 batch (per rank), resident in HBM
@@ -274,12 +479,15 @@ def main():
     plan = _lib.AlignPlan(batch)
     host_s, dev_s = time_steps(plan, args.steps, args.warmup, dist_on)
     step_s = max(host_s, dev_s) / args.steps
-    t = torch.tensor([step_s], dtype=torch.float64, device=device)
-    if dist_on:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    step_s = float(t.item())
+    step_s = _allreduce([step_s], "max")[0] if dist_on else step_s
     audio_per_step = float(sum(batch.Ts)) * FRAME_S * world  # seconds of audio aligned per step, all ranks
     value = audio_per_step / step_s
+    corpus = None
+    if not args.no_corpus:
+        try:
+            corpus = corpus_config4(device, rank, world, dist_on)
+        except Exception as e:  # never let the secondary leg hide the primary line
+            corpus = {"error": repr(e)[:300]}
 
     out = None
     if rank == 0:
@@ -316,6 +524,8 @@ def main():
         out["mae_ms"] = mae
         out["mae_detail"] = {"tokens": ntok, "segments_with_path_mismatch": nbad, "vs": "CPU oracle, same emission"}
         extra = {}
+        if corpus is not None:
+            extra["config4_10h_corpus"] = corpus
         if not args.no_scale and world == 1:
             # saturated batch: enough segments in flight to fill the chip (roofline regime)
             rng2 = np.random.default_rng(77)
@@ -382,7 +592,19 @@ def main():
             ems_cpu = [e.cpu() for e in ems]
             out["cpu_baseline"] = cpu_port_baseline(ems_cpu, toks)
             extra["cpu_c_oracle"] = c_oracle_baseline([e.numpy() for e in ems_cpu], toks)
-            extra["host_cpu"] = {"os_cpu_count": os.cpu_count(), "model": _cpu_model()}
+            extra["host_cpu"] = {"os_cpu_count": os.cpu_count(), "usable_threads": _host_threads(),
+                                 "model": _cpu_model()}
+            try:
+                extra["cpu_align_config1"] = {
+                    "all_threads": cpu_align_baseline(_host_threads()),
+                    "one_thread": cpu_align_baseline(1, budget_s=15.0),
+                    "kind": "port", "model": "random-weight wav2vec2-base (WAV2VEC2_ASR_BASE_960H architecture)",
+                    "sample": "config 1: one 30 s clip, T=1499, ~70 words, CPU forward + TorchPort DP + host "
+                              "aggregation, repeated for ~15-20 s; all_threads = the cores this process may "
+                              "use (sched_getaffinity, capped by OMP_NUM_THREADS), not os.cpu_count(): on a "
+                              "shared box os.cpu_count() counts the whole machine and oversubscribes"}
+            except Exception as e:
+                extra["cpu_align_config1"] = {"error": repr(e)[:300]}
         if not args.no_e2e and world == 1:
             try:
                 extra["e2e_align"] = e2e_align(device)
@@ -392,12 +614,34 @@ def main():
                 extra["e2e_config3_1h"] = e2e_config3(device)
             except Exception as e:
                 extra["e2e_config3_1h"] = {"error": repr(e)[:200]}
+            try:
+                me = mae_e2e(device)
+                out["mae_e2e_ms"] = me["mae_ms"]
+                extra["mae_e2e"] = me
+            except Exception as e:
+                extra["mae_e2e"] = {"error": repr(e)[:300]}
+            ca = extra.get("cpu_align_config1", {}).get("all_threads", {})
+            ea = extra.get("e2e_align", {})
+            if "value" in ca and "value" in ea:
+                extra["north_star_ratio"] = {
+                    "gpu_align_audio_sec_per_s": ea["value"], "cpu_align_audio_sec_per_s": ca["value"],
+                    "cpu_threads": ca["threads"], "ratio": ea["value"] / ca["value"], "target": 50.0,
+                    "note": "align() end to end on 1 MI355X (GPU forward + fused DP) over the reference-structured "
+                            "CPU align() on every usable host thread, same model architecture and clip length"}
         out["extra"] = extra
     if dist_on:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def _host_threads():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
 
 
 def _cpu_model():

@@ -1,0 +1,92 @@
+"""Whole-pipeline GPU tests (-m gpu):
+
+* BASELINE config 4 at full size on one GPU (world_size 1): the 10 h, 40-file synthetic corpus
+  through the per-file pipeline transcribe.py:172-205 runs file after file -- GPU
+  merge_chunks (vad.py:264-311) -> chunk bounds rounded to 3 dp (asr.py:226-232) -> align()
+  (alignment.py:100-354).  Every file's chunks must equal the oracle's Binarize + greedy merge,
+  and the fused DP inside align() must equal the oracle DP on the very emissions align()
+  produced, for every chunk.
+* The real emission path (north_star: word times within one 20 ms frame of the reference CPU
+  path): one random-weight wav2vec2-base, the same audio, forwarded on the GPU inside align()
+  and on the CPU through the reference-structured CPU align() path.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+
+
+def test_config4_corpus_pipeline_full_size_vs_oracle():
+    import whisperx_amd
+    from whisperx_amd import alignment, synthetic
+    from whisperx_amd.distributed import shard_files
+    from whisperx_amd.vad import merge_chunks
+
+    durs = synthetic.corpus_durations(4)
+    assert len(durs) == 40 and abs(sum(durs) - 36000.0) < 1.0
+    assert shard_files(durs, 1) == [list(range(40))]
+    dev = torch.device("cuda", 0)
+    model = synthetic.SyntheticCTC(V=32, seed=4).to(dev)
+    meta = {"language": "en", "dictionary": synthetic.w2v_dictionary(), "type": "huggingface"}
+    g = torch.Generator().manual_seed(4)
+    audio_buf = torch.randn(int(max(durs) * 16000) + 16000, generator=g) * 0.1
+    tr = synthetic.Transcriber(4)
+
+    captured = []
+    real_run_dp = alignment._run_dp
+
+    def spy(ems, toks, blanks, d):
+        res = real_run_dp(ems, toks, blanks, d)
+        captured.append(([e.cpu().numpy() for e in ems], toks, blanks, res))
+        return res
+
+    n_chunks = n_checked = n_words = 0
+    alignment._run_dp = spy
+    try:
+        for i, dur in enumerate(durs):
+            scores = synthetic.vad_scores(4000 + i, dur)
+            chunks = merge_chunks(scores, 30, 0.5, 0.363)
+            sw = scores.sliding_window
+            regions = oracle.binarize(scores.data[:, 0], sw.start, sw.step, sw.duration, 0.5, 0.363, 30)
+            ref = oracle.merge_chunks_regions(regions, 30)
+            assert [(c["start"], c["end"]) for c in chunks] == [(c["start"], c["end"]) for c in ref], f"file {i}"
+            assert [c["segments"] for c in chunks] == [c["segments"] for c in ref], f"file {i}"
+            segs = tr.segments(chunks)
+            assert all(s["start"] == round(c["start"], 3) and s["end"] == round(c["end"], 3)
+                       for s, c in zip(segs, chunks))
+            out = whisperx_amd.align(segs, model, meta, audio_buf[: int(dur * 16000)], dev)
+            n_chunks += len(segs)
+            n_words += len(out["word_segments"])
+            ems, toks, blanks, res = captured.pop()
+            assert len(ems) == len(segs)
+            for k in range(0, len(ems), 3):  # every third chunk of every file
+                ok, ts, ss, se, sc = oracle.align_dp(ems[k], toks[k], blanks[k])
+                g_ok, g_ss, g_se, g_sc, T = res[k]
+                assert bool(g_ok) == ok, (i, k)
+                assert T == ems[k].shape[0]
+                if ok:
+                    assert np.array_equal(g_ss, ss) and np.array_equal(g_se, se), (i, k)
+                    np.testing.assert_allclose(g_sc, sc, rtol=2.5e-7, atol=0)
+                n_checked += 1
+    finally:
+        alignment._run_dp = real_run_dp
+    assert n_chunks > 1000 and n_checked > 300 and n_words > 50_000
+    print(f"config 4: 40 files, {n_chunks} chunks, {n_words} words, {n_checked} chunk DPs checked")
+
+
+def test_real_emission_path_word_times_vs_cpu_reference_path():
+    import bench
+
+    r = bench.mae_e2e(torch.device("cuda", 0), n_seg=3, seed=7)
+    print("emission-path parity:", r)
+    assert r["words"] > 150
+    assert r["mae_ms"] <= 20.0, r  # north_star: within one 20 ms frame
