@@ -91,11 +91,21 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
  * (never materialised), argmax, backtrack and merge_repeats.  Outputs are CSR by tok_off:
  * seg_start/seg_end (frames, end exclusive) and seg_score of token k (the k-th
  * merge_repeats segment; a successful path always yields exactly N_s of them).
- * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None),
- * 2 not computed: V > 64 and the segment uses more than WX_MAX_SEGMENT_COLUMNS distinct
- * emission columns, 3 not computed: a split segment's cross-CU hand-off timed out (only
- * if another kernel starves the segment's CUs for ~0.1 s; re-run the call).
- * min_N/max_N/sum_T describe the batch (host values). */
+ * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None).
+ * Segments the fast kernels cannot finish are recomputed in-kernel by a generic (slow,
+ * barrier-per-step) forward with the same arithmetic: a split segment whose cross-CU
+ * hand-off timed out, and a V > 64 segment using more than WX_MAX_SEGMENT_COLUMNS distinct
+ * emission columns.  Only when that forward's LDS rows cannot hold the segment either
+ * (3 (N + 1) floats > ~84 KB, i.e. N > ~7000 such tokens) is the segment reported
+ * 2 (too many columns) or 3 (hand-off lost) and left uncomputed.
+ * min_N/max_N/sum_T describe the batch (host values).
+ * Split launches hand halo cells between CUs through a hand-off region of tagged granules
+ * and per-segment arrival counters.  wx_align_dp / wx_align_dp_mode carve it out of the
+ * workspace and zero it on the stream before the launch (hipMemsetAsync);
+ * wx_align_dp_ex takes a separate, caller-owned region instead, which must be all zero
+ * before its first use: every launch leaves it all zero again, so no per-launch memset is
+ * needed.  One hand-off region must not be used by two launches that may run at the same
+ * time (e.g. on two streams). */
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,
                 const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
@@ -130,6 +140,19 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V,
                      int32_t* seg_start, int32_t* seg_end, double* seg_score,
                      int32_t* t_start, int32_t* status,
                      void* workspace, size_t workspace_bytes, int32_t mode, void* stream);
+
+/* Bytes of the hand-off region wx_align_dp_ex needs for a batch (0 < result; caller-owned,
+ * zeroed once before first use). */
+size_t wx_align_dp_handoff_bytes(int32_t S, int64_t sum_T);
+/* wx_align_dp_mode with a caller-owned hand-off region (see wx_align_dp above).  handoff
+ * may be NULL: then the region is carved out of the workspace and zeroed per launch. */
+int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V,
+                   const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
+                   int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T,
+                   int32_t* seg_start, int32_t* seg_end, double* seg_score,
+                   int32_t* t_start, int32_t* status,
+                   void* workspace, size_t workspace_bytes,
+                   void* handoff, size_t handoff_bytes, int32_t mode, void* stream);
 
 /* Diagnostics (no device work): the kernels wx_align_dp_mode would launch for a batch of S
  * segments with token counts in [min_N, max_N] and vocabulary size V, written to buf as a

@@ -197,21 +197,65 @@ def test_align_dp_large_vocabulary_vs_oracle(V, mode):
     _check_vs_oracle(cases, f"V{V} mode {mode}", mode)
 
 
-def test_align_dp_large_vocabulary_too_many_columns():
-    """More than 256 distinct columns in one segment: status 2 (not computed), neighbours fine."""
-    from whisperx_amd import _lib
-
+@pytest.mark.parametrize("mode", MODES)
+def test_align_dp_large_vocabulary_too_many_columns(mode):
+    """More than 256 distinct columns in one segment: the compact LDS row cannot hold them,
+    so the segment is recomputed in-kernel by the generic forward (status 2 before round 2);
+    results equal the oracle, neighbours unaffected."""
     rng = np.random.default_rng(9)
     ok_cases = _large_vocab_cases(rng, 1000, 2, (600, 700), (100, 200), 40)
-    big = _large_vocab_cases(rng, 1000, 1, (900, 1000), (600, 700), 400)
-    cases = [ok_cases[0], big[0], ok_cases[1]]
+    big = _large_vocab_cases(rng, 1000, 2, (900, 1000), (600, 700), 400)
+    tie = _large_vocab_cases(rng, 1000, 1, (300, 400), (280, 290), 300)
+    tie[0]["em"] = (np.round(tie[0]["em"] * 16) / 16).astype(np.float32)  # exact ties
+    nofit = _large_vocab_cases(rng, 1000, 1, (10, 40), (300, 320), 300)  # N > T: backtrack fails
+    _check_vs_oracle([ok_cases[0], big[0], ok_cases[1], big[1], tie[0], nofit[0]], f"many columns mode {mode}", mode)
+
+
+def test_align_dp_lost_handoff_recovered(monkeypatch):
+    """A split segment whose cross-CU hand-off is lost (WX_SPIN_LIMIT=0: no consumer part
+    waits for its predecessor) is recomputed in-kernel by the last part to arrive; results
+    still equal the oracle, in the auto (split) shape and every explicit split."""
+    rng = np.random.default_rng(12)
+    cases = _random_cases(rng, 12, (1400, 1600), (300, 500), 32)
+    cases += _random_cases(rng, 2, (2900, 3000), (850, 950), 32)
+    cases += _random_cases(rng, 2, (20, 200), (10, 60), 32, quant=16)
+    monkeypatch.setenv("WX_SPIN_LIMIT", "0")
+    for mode in (-1, 12, 13, 14):
+        _check_vs_oracle(cases, f"lost hand-offs mode {mode}", mode)
+    monkeypatch.delenv("WX_SPIN_LIMIT")
+    _check_vs_oracle(cases, "after recovery", -1)
+
+
+def test_align_dp_handoff_region_left_zeroed():
+    """wx_align_dp_ex: a split launch leaves its caller-owned hand-off region all zero (the
+    contract that lets callers skip a per-launch memset), and foreign data in a fresh
+    workspace-carved region cannot leak into results (wx_align_dp_mode zeroes it)."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(13)
+    cases = _random_cases(rng, 16, (1400, 1600), (300, 500), 32)
     b = _batch(cases)
-    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b))
-    assert list(st) == [0, 2, 0]
-    for s_, c in ((0, cases[0]), (2, cases[2])):
+    plan = _lib.AlignPlan(b, mode=14)
+    for _ in range(3):
+        plan.run()
+    torch.cuda.synchronize()
+    assert int(plan.ho.count_nonzero()) == 0
+    # a workspace full of tag-like garbage through the memset path
+    lib = _lib.load()
+    wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
+    ws = torch.full((wsb // 8 + 1,), -1, dtype=torch.int64, device=DEV)
+    outs = [torch.empty(max(b.tok_off[-1], 1), dtype=t, device=DEV) for t in (torch.int32, torch.int32, torch.float64)]
+    ts = torch.empty(b.S, dtype=torch.int32, device=DEV)
+    st = torch.empty(b.S, dtype=torch.int32, device=DEV)
+    _lib._check(lib.wx_align_dp_mode(_lib._ptr(b.em), _lib._ptr(b.em_off_d), b.V, _lib._ptr(b.tok),
+                                     _lib._ptr(b.tok_off_d), _lib._ptr(b.blank), b.S, b.min_N, b.max_N, b.sum_T,
+                                     *[_lib._ptr(o) for o in outs], _lib._ptr(ts), _lib._ptr(st), _lib._ptr(ws), wsb,
+                                     14, _lib._stream(torch.device(DEV))))
+    ss, se = outs[0].cpu().numpy(), outs[1].cpu().numpy()
+    for s_, c in enumerate(cases):
         ok, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
         a, e = b.tok_off[s_], b.tok_off[s_ + 1]
-        assert ok and ts[s_] == tso and np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo)
+        assert ok and int(st[s_]) == 0 and np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo)
 
 
 def test_trellis_large_vocabulary_vs_oracle():

@@ -45,6 +45,9 @@ SIGNATURES = {
                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "wx_align_dp_mode": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _sz, _i32, _vp]),
+    "wx_align_dp_handoff_bytes": (_sz, [_i32, _i64]),
+    "wx_align_dp_ex": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
+                                      _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _i32, _vp]),
     "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
@@ -139,6 +142,26 @@ class Workspace:
 
 
 _ws = Workspace()
+
+
+class Handoff:
+    """Zero-initialised hand-off regions of split launches (wx_align_dp_ex), one per (device,
+    stream): every launch leaves its region all zero, so it is zeroed only when allocated or
+    grown; two streams never share one (concurrent launches must not)."""
+
+    def __init__(self):
+        self.buf: dict = {}
+
+    def get(self, device, stream_handle: int, nbytes: int) -> torch.Tensor:
+        key = (str(device), int(stream_handle))
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_handoff = Handoff()
 
 
 # ----------------------------------------------------------------------------------- batch
@@ -236,11 +259,14 @@ def align_dp(b: Batch, mode: int = MODE_AUTO):
     status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
     wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
     ws = _ws.get(dev, wsb)
+    hob = lib.wx_align_dp_handoff_bytes(b.S, b.sum_T)
     with torch.cuda.device(dev):
-        _check(lib.wx_align_dp_mode(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d),
-                                    _ptr(b.blank), b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end),
-                                    _ptr(seg_score), _ptr(t_start), _ptr(status), _ptr(ws), wsb, int(mode),
-                                    _stream(dev)))
+        stream = torch.cuda.current_stream(dev)
+        ho = _handoff.get(dev, stream.cuda_stream, hob)
+        _check(lib.wx_align_dp_ex(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d),
+                                  _ptr(b.blank), b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end),
+                                  _ptr(seg_score), _ptr(t_start), _ptr(status), _ptr(ws), wsb, _ptr(ho), ho.numel(),
+                                  int(mode), ctypes.c_void_p(stream.cuda_stream)))
     return seg_start, seg_end, seg_score, t_start, status
 
 
@@ -262,13 +288,17 @@ class AlignPlan:
         self.status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
         self.wsb = self.lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
         self.ws = torch.empty(max(self.wsb, 1), dtype=torch.uint8, device=dev)
+        # the plan's own hand-off region (zeroed once; its launches keep it zeroed); runs of
+        # one plan are serialised by the caller (one stream at a time)
+        self.hob = self.lib.wx_align_dp_handoff_bytes(b.S, b.sum_T)
+        self.ho = torch.zeros(max(self.hob, 1), dtype=torch.uint8, device=dev)
         self.args = (_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S,
                      b.min_N, b.max_N, b.sum_T, _ptr(self.seg_start), _ptr(self.seg_end), _ptr(self.seg_score),
-                     _ptr(self.t_start), _ptr(self.status), _ptr(self.ws), self.wsb)
+                     _ptr(self.t_start), _ptr(self.status), _ptr(self.ws), self.wsb, _ptr(self.ho), self.hob)
 
     def run(self, stream=None):
         st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.b.device).cuda_stream)
-        _check(self.lib.wx_align_dp_mode(*self.args, self.mode, st))
+        _check(self.lib.wx_align_dp_ex(*self.args, self.mode, st))
         return self.seg_start, self.seg_end, self.seg_score, self.t_start, self.status
 
 

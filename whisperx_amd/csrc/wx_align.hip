@@ -372,6 +372,7 @@ struct Split {
     uint64_t* xin;    // granules from part p-1: [chunk][kHaloCells] (p > 0)
     uint64_t* xout;   // granules to part p+1 (p < P-1)
     int xstride;      // granules per chunk block of one segment boundary
+    int spin;         // re-reads before a hand-off counts as lost (kMaxSpin; 0 in the recovery test)
 };
 
 __device__ __forceinline__ void granule_store(uint64_t* g, float v, unsigned tag) {
@@ -436,7 +437,7 @@ struct Forward {
     // SP: make xpre[] hold chunk q's halo granules (lanes < HL, C each), re-reading until
     // every tag matches.  Returns whether they were already there; bounded (sets lost).
     __device__ __forceinline__ static bool xwait(const uint64_t* xin, int xstride, int q, int l, unsigned tag,
-                                                 uint64_t (&xpre)[C], bool& lost) {
+                                                 uint64_t (&xpre)[C], bool& lost, int spin) {
         constexpr int HL = Geometry<C, 2>::HL;
         const unsigned want = tag | (unsigned)(q & 0xFFF);
         const uint64_t* gi = xin + (int64_t)q * xstride + min(l, HL - 1) * C;  // all lanes load
@@ -444,7 +445,7 @@ struct Forward {
 #pragma unroll
         for (int k = 0; k < C; ++k) ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
         const bool first = __all(ok);
-        for (int it = 0; !lost && !__all(ok) && it < kMaxSpin; ++it) {
+        for (int it = 0; !lost && !__all(ok) && it < spin; ++it) {
             __builtin_amdgcn_s_sleep(2);
             ok = true;
 #pragma unroll
@@ -609,7 +610,7 @@ struct Forward {
                 // marks the segment failed.  (An LDS-DMA landing ring with hand-counted vmcnt
                 // measured no better.)
                 WX_T(x0);
-                const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost);
+                const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost, sp->spin);
                 if (l < Geo::HL) {
 #pragma unroll
                     for (int k = 0; k < C; ++k) st.cur[k] = __builtin_bit_cast(float, (unsigned)xpre[k]);
@@ -619,7 +620,7 @@ struct Forward {
                     uint64_t tmp[C];
 #pragma unroll
                     for (int k = 0; k < C; ++k) tmp[k] = 0;
-                    xwait(sp->xin, sp->xstride, q + kXSlack, l, sp->tag, tmp, xlost);
+                    xwait(sp->xin, sp->xstride, q + kXSlack, l, sp->tag, tmp, xlost, sp->spin);
                 }
 #ifdef WX_PHASE_TIMING
                 WX_T(x2);
@@ -996,6 +997,65 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
         }
     }
     return uniform(nan_row != 0x7fffffff ? nan_row : best_row);
+}
+
+// ------------------------------------------------------------------------------------
+// Generic forward of one segment by the whole workgroup: one time step per barrier, cells
+// strided over the threads, rows ping-ponged in LDS.  Orders of magnitude slower than
+// Forward (~1-3 ms per 30 s segment) and used only to recover a segment the fast path could
+// not finish: a split segment whose cross-CU hand-off timed out (status 3 before round 2)
+// and a large-vocabulary segment with more than kGatherVS distinct columns (status 2 before
+// round 2).  Same arithmetic as Forward::advance (alignment.py:367-378: fp32 adds, strict
+// `changed > stayed` bit, NaN-propagating max, fp64 column-0 cumsum, +inf in the last N rows
+// of column 0) and the same outputs in the same places: the decision words in the launch's
+// bitmap layout `lay`, the column-N history cn[0..T-1] and q0.  Returns false (nothing
+// written) when two rows plus the decision words of N cells do not fit in `lds_floats`.
+__device__ __noinline__ bool generic_forward(int T, int N, int blank, const float* __restrict__ E, int V,
+                                             const int32_t* __restrict__ tok /* segment's tokens */,
+                                             unsigned* __restrict__ bits, Layout lay, float* __restrict__ cn,
+                                             float* __restrict__ q0, float* lds, int lds_floats) {
+    if (3 * (N + 1) > lds_floats) return false;
+    float* ra = lds;
+    float* rb = lds + (N + 1);
+    unsigned* wb = reinterpret_cast<unsigned*>(lds + 2 * (N + 1));  // wb[j-1]: cell j's open word
+    const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
+    const int inf_from = T + 1 - N;
+    for (int j = tid; j <= N; j += nthr) {
+        ra[j] = j == 0 ? col0_value(0, 0.0, T, N) : -INFINITY;
+        if (j > 0) wb[j - 1] = 0u;
+    }
+    for (int t = tid; t < T; t += nthr) q0[t] = exp_cr(E[(int64_t)t * V]);
+    double acc = 0.0;  // sum of em[0..t, 0] (every thread, same order)
+    for (int t = 0; t < T; ++t) {
+        __syncthreads();
+        const float* row = E + (int64_t)t * V;
+        const float eb = row[blank];
+        const bool flush = (t & (kChunk - 1)) == kChunk - 1 || t == T - 1;
+        const int sh = kChunk - 1 - (t & (kChunk - 1));  // keep bit 31 = first step of the block
+        for (int j = tid + 1; j <= N; j += nthr) {
+            int tk = tok[j - 1];
+            tk = (tk >= 0 && tk < V) ? tk : 0;
+            const float s = ra[j] + eb;
+            const float c = ra[j - 1] + row[tk];
+            unsigned w = (wb[j - 1] << 1) | (c > s ? 1u : 0u);
+            rb[j] = nan_max(s, c);
+            if (j == N) cn[t] = rb[j];
+            if (flush) {
+                int g, k;
+                lay.locate(j - 1, g, k);
+                bits[((int64_t)(t >> 5) * lay.C + k) * lay.lanes + g] = w << sh;
+                w = 0u;
+            }
+            wb[j - 1] = w;
+        }
+        acc += (double)row[0];
+        if (tid == 0) rb[0] = (t + 1 >= inf_from) ? INFINITY : (float)acc;
+        float* x = ra;
+        ra = rb;
+        rb = x;
+    }
+    __syncthreads();
+    return true;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1376,6 +1436,7 @@ struct AlignArgs {
     unsigned epoch;  // split launches: per-launch tag of the hand-off granules and counters
     uint64_t* xg;    // workspace: hand-off granules, (floor(row0/32) + seg + q) * 3 * 40
     unsigned* arrive;// workspace: per-segment arrival counters (epoch << 8 | count)
+    int spin;        // split launches: hand-off re-reads before a part counts as lost
 };
 
 // Per-segment arrival of a split segment's parts; true for the last to arrive.  The word
@@ -1393,6 +1454,15 @@ __device__ unsigned split_arrive(unsigned* c, unsigned epoch, bool lost) {
     }
 }
 
+
+// Zero a split segment's hand-off granules (nch chunk blocks of `stride` granules) with the
+// threads [first_thread, blockDim): a launch leaves its hand-off region as it found it, all
+// zero, so no stale or foreign word can ever carry a valid tag (include/wx_align.h).
+__device__ __forceinline__ void clear_handoff(uint64_t* xseg, int nch, int stride, int first_thread = 0) {
+    const int n = (int)blockDim.x - first_thread;
+    const int64_t total = (int64_t)nch * stride;
+    for (int64_t i = (int)threadIdx.x - first_thread; i < total; i += n) xseg[i] = 0ull;
+}
 
 // Latency buckets (H) claim more than half of a CU's 160 KB LDS so that the dispatcher
 // places one workgroup per CU: two 8-wave workgroups on one CU would share its SIMDs
@@ -1454,13 +1524,10 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         return;
     }
     ColMap cm;
-    if (!prepare_colmap(cml, cm, a.tok + d.tok0, d.N, d.blank, a.V)) {
-        if (lane == 0 && part == 0) {
-            a.t_start[seg] = 0;
-            a.status[seg] = 2;  // more than kGatherVS distinct columns in one segment
-        }
-        return;
-    }
+    // More than kGatherVS distinct columns: the compact LDS row cannot hold the segment's
+    // emissions, so one workgroup (part 0 of a split) runs the generic forward instead.
+    const bool slow = !prepare_colmap(cml, cm, a.tok + d.tok0, d.N, d.blank, a.V);
+    if (slow && part != 0) return;
     const float* E = a.em + d.row0 * a.V;
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
@@ -1468,25 +1535,29 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     WX_STAMP_RT(4);
     WX_STAMP(0);
     Split sp;
+    uint64_t* xseg = nullptr;  // SP: this segment's granule block
     if (SP) {
         sp.p = part;
         sp.P = P;
         sp.lanes = kWave * W * P;
         sp.tag = a.epoch << 12;
         sp.xstride = (kMaxParts - 1) * kHaloCells;
-        uint64_t* xs = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
-        sp.xin = xs + (part > 0 ? part - 1 : 0) * kHaloCells;
-        sp.xout = xs + part * kHaloCells;
+        sp.spin = a.spin;
+        xseg = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
+        sp.xin = xseg + (part > 0 ? part - 1 : 0) * kHaloCells;
+        sp.xout = xseg + part * kHaloCells;
     }
     if (SP && lane == 0) tsb[2] = 0;
-    const bool lost = Forward<C, VS, 0, W, H != 0, SP>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
-                                                            a.x4 != 0, cm, nullptr, &sp);
+    bool lost = false;
+    if (!slow)
+        lost = Forward<C, VS, 0, W, H != 0, SP>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
+                                                     a.x4 != 0, cm, nullptr, &sp);
     WX_STAMP(1);
     if (SP && lost) tsb[2] = 1;  // (any lane of wave 0)
     wait_vm();
     block_fence();
     bool failed = false;
-    if (SP) {  // release this part's bits / column-N history; the last part to arrive goes on
+    if (SP && !slow) {  // release this part's bits / column-N history; the last part to arrive goes on
         if (lane == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             wait_vm();
@@ -1495,6 +1566,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
             if (tsb[0]) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 wait_vm();
+                // every part has arrived: leave the counter clean for the next launch
+                __hip_atomic_store(a.arrive + seg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
@@ -1506,6 +1579,21 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         }
         failed = tsb[0] == 2;
         __syncthreads();
+    }
+    const Layout lay = Layout::make(C, d.N, kWave * W * P);
+    if (slow || failed) {
+        // recovery: a lost hand-off (some part computed with a stale halo) or a segment whose
+        // columns do not fit the compact row.  The whole workgroup recomputes the segment.
+        if (!generic_forward(d.T, d.N, d.blank, E, a.V, a.tok + d.tok0, bits, lay, cn, q0, lds, kLdsFloats)) {
+            if (lane == 0) {
+                a.t_start[seg] = 0;
+                a.status[seg] = slow ? 2 : 3;  // (N too large for the generic forward's LDS rows)
+            }
+            if (SP) clear_handoff(xseg, (d.T + kChunk - 1) / kChunk, (kMaxParts - 1) * kHaloCells);
+            return;
+        }
+        wait_vm();
+        block_fence();
     }
     int32_t* start = a.seg_start + d.tok0;
 #ifdef WX_PHASE_TIMING
@@ -1521,7 +1609,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
             tsb[0] = ts;
         }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk<C>(bits, Layout::make(C, d.N, kWave * W * P), d.N, ts, cmask, d.T <= kMaxLdsFrames);
+        const int b_lo = walk<C>(bits, lay, d.N, ts, cmask, d.T <= kMaxLdsFrames);
 #ifdef WX_PHASE_TIMING
         WX_T(w2);
 #endif
@@ -1539,16 +1627,18 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
             o[2] = w3 - w2;
         }
 #endif
-    } else if (H) {
-        fill_q0(E, a.V, d.T, q0, kWave);
+    } else {
+        if (H && !slow && !failed) fill_q0(E, a.V, d.T, q0, kWave);
+        // the segment's hand-off granules are consumed: zero them for the next launch
+        if (SP && !slow) clear_handoff(xseg, (d.T + kChunk - 1) / kChunk, (kMaxParts - 1) * kHaloCells, kWave);
     }
     wait_vm();
     block_fence();
     const int ts = tsb[0];
     const bool ok = tsb[1] != 0;
     WX_STAMP(2);
-    if (lane == 0) a.status[seg] = failed ? 3 : (ok ? 0 : 1);
-    if (!ok || failed) return;
+    if (lane == 0) a.status[seg] = ok ? 0 : 1;
+    if (!ok) return;
     merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
     WX_STAMP(3);
     WX_STAMP_RT(5);
@@ -2214,10 +2304,21 @@ int split_parts(int32_t S, int mode, int32_t requested) {
     return std::max(1, std::min(want, fit)) >= 2 ? std::max(1, std::min(want, fit)) : 1;
 }
 
-unsigned next_epoch() {
+unsigned next_epoch() {  // never 0: a zeroed granule or counter carries no valid tag
     static std::atomic<unsigned> e{(unsigned)std::chrono::steady_clock::now().time_since_epoch().count()};
-    return (e.fetch_add(1) + 1) & 0xFFFFFu;
+    const unsigned v = (e.fetch_add(1) + 1) & 0xFFFFFu;
+    return v ? v : 1u;
 }
+
+// Hand-off re-reads before a split part gives up on a granule.  WX_SPIN_LIMIT (read per call)
+// lowers it; 0 forces every consumer to lose its hand-offs (the recovery test).
+static int spin_limit() {
+    const char* e = getenv("WX_SPIN_LIMIT");
+    if (e && e[0] >= '0' && e[0] <= '9') return std::min(atoi(e), kMaxSpin);
+    return kMaxSpin;
+}
+
+size_t wx_align_dp_handoff_bytes(int32_t S, int64_t sum_T) { return xg_bytes(S, sum_T) + arrive_bytes(S); }
 
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok, const int64_t* tok_off,
                 const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N, int64_t sum_T, int32_t* seg_start,
@@ -2231,6 +2332,15 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
                      const int64_t* tok_off, const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N,
                      int64_t sum_T, int32_t* seg_start, int32_t* seg_end, double* seg_score, int32_t* t_start,
                      int32_t* status, void* workspace, size_t workspace_bytes, int32_t mode, void* stream) {
+    return wx_align_dp_ex(em, em_off, V, tok, tok_off, blank_id, S, min_N, max_N, sum_T, seg_start, seg_end,
+                          seg_score, t_start, status, workspace, workspace_bytes, nullptr, 0, mode, stream);
+}
+
+int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int32_t* tok,
+                   const int64_t* tok_off, const int32_t* blank_id, int32_t S, int64_t min_N, int64_t max_N,
+                   int64_t sum_T, int32_t* seg_start, int32_t* seg_end, double* seg_score, int32_t* t_start,
+                   int32_t* status, void* workspace, size_t workspace_bytes, void* handoff, size_t handoff_bytes,
+                   int32_t mode, void* stream) {
     if (!(mode >= WX_MODE_AUTO && mode <= WX_MODE_LATENCY_1CU) && !(mode >= WX_MODE_SPLIT2 && mode <= WX_MODE_SPLIT4))
         return WX_E_INVALID;
     if (S < 0 || sum_T < 0 || min_N < 0 || max_N < min_N) return WX_E_INVALID;
@@ -2241,6 +2351,7 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
     if (V < 1 || V > WX_MAX_VOCAB) return WX_E_VOCAB;
     if (max_N > WX_MAX_TOKENS) return WX_E_TOO_LONG;
     if (workspace_bytes < wx_align_dp_workspace_bytes(S, sum_T, max_N)) return WX_E_WORKSPACE;
+    if (handoff && handoff_bytes < wx_align_dp_handoff_bytes(S, sum_T)) return WX_E_WORKSPACE;
     AlignArgs a;
     a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id; a.S = S;
     a.seg_start = seg_start; a.seg_end = seg_end; a.seg_score = seg_score; a.t_start = t_start; a.status = status;
@@ -2250,12 +2361,17 @@ int wx_align_dp_mode(const float* em, const int64_t* em_off, int32_t V, const in
     a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
                                           align_up((size_t)(sum_T + 1) * 4u, 256));
     a.cn = reinterpret_cast<float*>(reinterpret_cast<char*>(a.cmask) + cmask_bytes(S, sum_T));
-    a.xg = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
+    a.xg = reinterpret_cast<uint64_t*>(handoff ? handoff : reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
     a.arrive = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.xg) + xg_bytes(S, sum_T));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a.mode = align_mode(S, mode);
     a.parts = split_parts(S, a.mode, mode);
     a.epoch = next_epoch();
+    a.spin = spin_limit();
+    if (a.parts > 1 && !handoff) {  // workspace hand-off region: holds anything until zeroed
+        const hipError_t e = hipMemsetAsync(a.xg, 0, wx_align_dp_handoff_bytes(S, sum_T), st);
+        if (e != hipSuccess) return (int)e;
+    }
     a.x4 = (V == 32 && (reinterpret_cast<uintptr_t>(em) & 15) == 0) ? 1 : 0;
     int ids[kNumBuckets + 8];
     a.split_id = a.parts > 1 ? split_launch_id(max_N, a.parts) : 0;
