@@ -237,6 +237,31 @@ def e2e_config3(device, seed=3):
                     "synthetic scores/audio/transcripts"}
 
 
+def vad_producer_1h(device, seed=5, batch_size=128):
+    """VAD producer (vad.py:198-240) on 1 h of audio: 7,191 five-second windows every 0.5 s
+    through the random-weight PyanNet-shaped segmentation model (batched) and the overlap-add
+    HIP kernel.  Timing only (random weights: merge_chunks over these scores is exercised by
+    tests/test_vad_producer.py; the config-3 leg binarises smooth synthetic scores)."""
+    from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+    torch.manual_seed(seed)
+    vad = VoiceActivitySegmentation(device=device, batch_size=batch_size)
+    g = torch.Generator().manual_seed(seed)
+    wav = torch.randn(1, 3600 * 16000, generator=g) * 0.1
+    wav_d = wav.to(device)
+    vad({"waveform": wav_d[:, : 120 * 16000], "sample_rate": 16000})  # warm-up (MIOpen, LSTM)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    feat = vad({"waveform": wav_d, "sample_rate": 16000})
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    n_win = sum(vad.windows(wav.shape[1]))
+    return {"audio_sec": 3600.0, "windows": int(n_win), "frames": int(feat.data.shape[0]),
+            "producer_ms": 1000 * (t1 - t0), "audio_sec_per_s": 3600.0 / (t1 - t0), "batch_size": batch_size,
+            "note": "PyanNet-shaped random-weight segmentation forward (fp32, 5 s windows every 0.5 s) + "
+                    "wx_vad_aggregate; scores left on the device for merge_chunks; audio resident on the GPU"}
+
+
 def _w2v_base(device, seed):
     """Random-weight wav2vec2-base (WAV2VEC2_ASR_BASE_960H's architecture, V=32): there are
     no checkpoints offline, and the forward's cost does not depend on the weights."""
@@ -610,6 +635,10 @@ def main():
                 extra["e2e_align"] = e2e_align(device)
             except Exception as e:  # never let the secondary leg hide the primary line
                 extra["e2e_align"] = {"error": repr(e)[:200]}
+            try:
+                extra["vad_producer_1h"] = vad_producer_1h(device)
+            except Exception as e:
+                extra["vad_producer_1h"] = {"error": repr(e)[:300]}
             try:
                 extra["e2e_config3_1h"] = e2e_config3(device)
             except Exception as e:

@@ -13,6 +13,8 @@
  *                        materialised; a 1-bit decision map replaces it for the backtrack.
  *   wx_binarize       <- whisperx/vad.py:118  Binarize.__call__ (hysteresis + min-cut),
  *                        the kernel under vad.py:264 merge_chunks
+ *   wx_vad_aggregate  <- whisperx/vad.py:198-240 VoiceActivitySegmentation.apply's
+ *                        segmentation overlap-add (pyannote Inference.aggregate)
  *
  * Conventions
  *   - All data pointers are DEVICE pointers (allocated by the caller; the library never
@@ -170,6 +172,16 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files,
                 float onset, float offset, double max_duration, double pad_onset, double pad_offset,
                 double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
                 void* stream);
+
+/* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
+ * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32
+ * (the segmentation model's sigmoid outputs per chunk), start_frame[c] = the file-grid frame
+ * where chunk c's first frame lands (non-decreasing).  out[f] = (sum over covering chunks, in
+ * chunk order, of max_k scores[c, f - start_frame[c], k]) / (number of them), NaN outputs
+ * masked out; `missing` where no chunk covers f.  Feeds wx_binarize on the device. */
+int wx_vad_aggregate(const float* scores, const int64_t* start_frame, int32_t n_chunks,
+                     int32_t frames_per_chunk, int32_t n_classes, int64_t n_frames, float missing,
+                     float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -208,3 +208,29 @@ class TorchPort:
         tr = self.trellis(em, tokens, blank)
         path = self.backtrack(tr, em, tokens, blank)
         return None if path is None else self.merge_repeats(path)
+
+
+def vad_aggregate(scores, start_frames, n_frames, missing=np.nan):
+    """The VAD producer's overlap-add (whisperx/vad.py:198-240 -> pyannote.audio 3.1.1
+    ``Inference.aggregate``, setup.py:23 pins pyannote.audio==3.1.1; pyannote is not installed
+    here, so this restates its published algorithm and is itself "parity unpinned"):
+    multi-label pre-aggregation hook ``np.max(scores, axis=-1, keepdims=True)``, then, with
+    hamming=False, warm_up=(0, 0), skip_average=False, window by window in order:
+    ``aggregated[s:s+K] += score * mask``, ``count[s:s+K] += mask``, ``seen = max(seen, mask)``
+    (float32 accumulators), ``aggregated / maximum(count, 1e-12)``, ``missing`` where unseen.
+    scores [n_chunks, K, n_classes]; returns [n_frames] float32."""
+    s = np.max(np.asarray(scores, np.float32), axis=-1, keepdims=True)
+    masks = 1 - np.isnan(s)
+    s = np.nan_to_num(s, copy=True, nan=0.0)
+    K = s.shape[1]
+    agg = np.zeros((n_frames, 1), np.float32)
+    cnt = np.zeros((n_frames, 1), np.float32)
+    seen = np.zeros((n_frames, 1), np.float32)
+    for c in range(s.shape[0]):
+        f0 = int(start_frames[c])
+        agg[f0:f0 + K] += (s[c] * masks[c])[: max(0, min(K, n_frames - f0))]
+        cnt[f0:f0 + K] += masks[c][: max(0, min(K, n_frames - f0))]
+        seen[f0:f0 + K] = np.maximum(seen[f0:f0 + K], masks[c][: max(0, min(K, n_frames - f0))])
+    avg = agg / np.maximum(cnt, 1e-12)
+    avg[seen == 0.0] = missing
+    return avg[:, 0]

@@ -1,0 +1,93 @@
+"""VAD producer (vad.py:198-240): the PyanNet-shaped segmentation model, pyannote's sliding
+windows and overlap-add geometry, and the wx_vad_aggregate kernel against the oracle
+restatement of pyannote.audio 3.1.1 Inference.aggregate (pyannote itself is absent: parity
+unpinned at the pyannote boundary; the kernel is pinned to the restatement bit for bit)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+
+def test_oracle_aggregate_hand_case():
+    # 3 windows of K=4 frames, 2 classes, starting at frames 0, 2, 3 (n_frames 8)
+    sc = np.array([[[0.1, 0.3], [0.2, 0.1], [0.5, np.nan], [0.4, 0.4]],
+                   [[0.9, 0.0], [0.1, 0.2], [np.nan, np.nan], [0.7, 0.6]],
+                   [[0.2, 0.2], [0.3, 0.1], [0.6, 0.6], [0.8, 0.9]]], np.float32)
+    out = oracle.vad_aggregate(sc, [0, 2, 3, 99][:3], 8, missing=-1.0)
+    m = np.max(sc, axis=-1)  # per window frame; a NaN class makes the frame NaN (masked)
+    exp = [m[0, 0], m[0, 1], (m[1, 0]) / 1, (m[0, 3] + m[1, 1] + m[2, 0]) / 3,
+           (m[2, 1]) / 1, (m[1, 3] + m[2, 2]) / 2, m[2, 3], -1.0]
+    # frame 2: window 0's value is NaN (masked), window 1 covers it with 0.9
+    exp[2] = np.float32(m[1, 0])
+    np.testing.assert_allclose(out, np.array(exp, np.float32), rtol=1e-6)
+    assert out[7] == -1.0
+
+
+def test_pyannet_geometry_and_windows():
+    from whisperx_amd.vad_model import PyanNet, VoiceActivitySegmentation, closest_frame
+
+    m = PyanNet()
+    assert PyanNet.n_frames(80000) == 293
+    assert round(m.frame_step * 16000) == 270 and round(m.frame_duration * 16000) == 991
+    with torch.no_grad():
+        y = m(torch.randn(2, 1, 80000))
+    assert y.shape == (2, 293, 3) and float(y.min()) >= 0 and float(y.max()) <= 1
+    v = VoiceActivitySegmentation.__new__(VoiceActivitySegmentation)
+    v.duration, v.step = 5.0, 0.5
+    assert v.windows(80000) == (1, False)
+    assert v.windows(80000 + 8000) == (2, False)
+    assert v.windows(80000 + 8001) == (2, True)
+    assert v.windows(1000) == (0, True)
+    # pyannote closest_frame: rint((t - start - d/2) / step)
+    assert closest_frame(0.5 + 0.5 * m.frame_duration, 0.0, m.frame_duration, m.frame_step) == round(0.5 / m.frame_step)
+
+
+@pytest.mark.gpu
+def test_vad_aggregate_kernel_vs_oracle():
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(5)
+    for n_chunks, K, C in ((50, 293, 3), (7, 20, 1), (1, 5, 2)):
+        sc = rng.random((n_chunks, K, C)).astype(np.float32)
+        sc[rng.random(sc.shape) < 0.02] = np.nan
+        sc[3 % n_chunks, :, :] = np.nan  # a fully masked window
+        starts = np.cumsum(np.concatenate([[0], rng.integers(0, K // 3 + 1, n_chunks - 1)]))
+        n_frames = int(starts[-1] + K + 3)  # a few frames no window covers
+        got = _lib.vad_aggregate(torch.from_numpy(sc).cuda(), starts.tolist(), n_frames).cpu().numpy()
+        exp = oracle.vad_aggregate(sc, starts, n_frames)
+        assert np.array_equal(got, exp, equal_nan=True), (n_chunks, K, C)
+
+
+@pytest.mark.gpu
+def test_vad_producer_end_to_end_device_scores():
+    """60 s of audio through the producer; its scores equal the oracle aggregation of its own
+    window outputs, and merge_chunks on the device-resident scores equals merge_chunks on a
+    host copy and the oracle Binarize + chunk merge."""
+    from whisperx_amd.vad import SlidingWindowFeature, merge_chunks
+    from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+    torch.manual_seed(0)
+    vad = VoiceActivitySegmentation(device="cuda:0", batch_size=16)
+    wav = torch.randn(1, 61 * 16000 + 123) * 0.1
+    feat = vad({"waveform": wav, "sample_rate": 16000})
+    assert feat.data.is_cuda and feat.data.shape[1] == 1
+    cs = vad.chunk_scores(wav).cpu().numpy()
+    n_full, has_last = vad.windows(wav.shape[1])
+    assert cs.shape == (n_full + int(has_last), 293, 3)
+    fd, fs = vad.model.frame_duration, vad.model.frame_step
+    from whisperx_amd.vad_model import closest_frame
+    starts = [closest_frame(c * 0.5 + 0.5 * fd, 0.0, fd, fs) for c in range(cs.shape[0])]
+    exp = oracle.vad_aggregate(cs, starts, feat.data.shape[0])
+    assert np.array_equal(feat.data[:, 0].cpu().numpy(), exp, equal_nan=True)
+    # a random-weight model's scores hover near one value: binarise around their median
+    med = float(np.nanmedian(exp))
+    dev_chunks = merge_chunks(feat, 30, onset=med, offset=med)
+    host = SlidingWindowFeature(feat.data.cpu().numpy(), feat.sliding_window)
+    assert dev_chunks == merge_chunks(host, 30, onset=med, offset=med)
+    sw = feat.sliding_window
+    regions = oracle.binarize(exp, sw.start, sw.step, sw.duration, med, med, 30)
+    ref = oracle.merge_chunks_regions(regions, 30)
+    assert [(c["start"], c["end"]) for c in dev_chunks] == [(c["start"], c["end"]) for c in ref]

@@ -49,6 +49,7 @@ SIGNATURES = {
     "wx_align_dp_ex": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                       _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _i32, _vp]),
     "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
+    "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
 }
@@ -89,7 +90,12 @@ def load(require_device: bool = True) -> ctypes.CDLL:
             raise WXError(f"{LIB_PATH} is missing: run whisperx_amd._lib.build() (hipcc, gfx950)")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if os.environ.get("WX_LIB_PATH"):  # an older build under A/B (tools/satbench.py)
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         _lib = lib
@@ -290,7 +296,7 @@ class AlignPlan:
         self.ws = torch.empty(max(self.wsb, 1), dtype=torch.uint8, device=dev)
         # the plan's own hand-off region (zeroed once; its launches keep it zeroed); runs of
         # one plan are serialised by the caller (one stream at a time)
-        self.hob = self.lib.wx_align_dp_handoff_bytes(b.S, b.sum_T)
+        self.hob = self.lib.wx_align_dp_handoff_bytes(b.S, b.sum_T) if hasattr(self.lib, "wx_align_dp_handoff_bytes") else 1
         self.ho = torch.zeros(max(self.hob, 1), dtype=torch.uint8, device=dev)
         self.args = (_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S,
                      b.min_N, b.max_N, b.sum_T, _ptr(self.seg_start), _ptr(self.seg_end), _ptr(self.seg_score),
@@ -298,7 +304,10 @@ class AlignPlan:
 
     def run(self, stream=None):
         st = ctypes.c_void_p(stream if stream is not None else torch.cuda.current_stream(self.b.device).cuda_stream)
-        _check(self.lib.wx_align_dp_ex(*self.args, self.mode, st))
+        if not hasattr(self.lib, "wx_align_dp_ex"):  # an older build under A/B
+            _check(self.lib.wx_align_dp_mode(*self.args[:-2], self.mode, st))
+        else:
+            _check(self.lib.wx_align_dp_ex(*self.args, self.mode, st))
         return self.seg_start, self.seg_end, self.seg_score, self.t_start, self.status
 
 
@@ -378,8 +387,13 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
     r_off = [0]
     for n in F:
         r_off.append(r_off[-1] + n + 1)
-    ys = torch.cat([torch.as_tensor(s, dtype=torch.float32).reshape(-1) for s in scores_list]) if F else torch.zeros(1)
-    ys = _h2d(ys, torch.float32, dev)
+    if F and all(torch.is_tensor(s) and s.is_cuda for s in scores_list):
+        # scores already on the device (the VAD producer's output): no host round trip
+        ys = torch.cat([s.to(device=dev, dtype=torch.float32).reshape(-1) for s in scores_list]).contiguous()
+    else:
+        ys = torch.cat([torch.as_tensor(s, dtype=torch.float32).reshape(-1).cpu() for s in scores_list]) \
+            if F else torch.zeros(1)
+        ys = _h2d(ys, torch.float32, dev)
     g = _h2d(torch.tensor(sw_geometry, dtype=torch.float64).reshape(-1, 3), torch.float64, dev)
     st0, stp, dur = g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].contiguous()
     rs = torch.empty(max(r_off[-1], 1), dtype=torch.float64, device=dev)
@@ -400,3 +414,18 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
             raise WXError("binarize region buffer overflow")
         out.append((rs_h[r_off[i]:r_off[i] + n], re_h[r_off[i]:r_off[i] + n]))
     return out
+
+
+def vad_aggregate(scores: torch.Tensor, start_frames, n_frames: int, missing: float = float("nan")):
+    """wx_vad_aggregate: scores [n_chunks, K, n_classes] fp32 device tensor, start_frames
+    (host ints, non-decreasing) -> [n_frames] fp32 device tensor."""
+    lib = load()
+    dev = scores.device
+    sc = scores.to(torch.float32).contiguous()
+    n_chunks, K, n_cls = (int(x) for x in sc.shape)
+    sf = _dev_i64(list(start_frames) if n_chunks else [0], dev)
+    out = torch.empty(max(int(n_frames), 1), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _check(lib.wx_vad_aggregate(_ptr(sc), _ptr(sf), n_chunks, K, n_cls, int(n_frames), float(missing),
+                                    _ptr(out), _stream(dev)))
+    return out[: int(n_frames)]

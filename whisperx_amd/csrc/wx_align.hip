@@ -2087,6 +2087,58 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
 
 // ======================================================================================
 // C ABI
+namespace wx {
+// ------------------------------------------------------------------------------------
+// VAD producer: overlap-add aggregation of the segmentation model's per-chunk frame scores
+// onto the file's frame grid (pyannote.audio Inference.aggregate, as called by
+// VoiceActivityDetection / whisperx's VoiceActivitySegmentation.apply, vad.py:198-240), with
+// the multi-label pre-aggregation hook (max over the model's speaker classes) fused in.
+// One thread per output frame gathers the chunks covering it in chunk order (the
+// reference's accumulation order: chunk by chunk, fp32 `+=`), so the result is deterministic
+// and equals the sequential numpy sum bit for bit.  Chunk c covers output frames
+// [start_frame[c], start_frame[c] + K); start_frame is non-decreasing.
+struct VadAggArgs {
+    const float* scores;        // [n_chunks, K, n_classes]
+    const int64_t* start_frame; // [n_chunks]
+    int n_chunks, K, n_classes;
+    int64_t n_frames;
+    float missing;              // value of frames no chunk covers (or all-NaN)
+    float* out;                 // [n_frames]
+};
+
+__global__ __launch_bounds__(256) void vad_aggregate_kernel(VadAggArgs a) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= a.n_frames) return;
+    // first chunk whose window can reach frame f: start_frame[c] > f - K (binary search)
+    int lo = 0, hi = a.n_chunks;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.start_frame[mid] <= f - a.K) lo = mid + 1;
+        else hi = mid;
+    }
+    float acc = 0.0f, cnt = 0.0f;
+    bool any = false;
+    for (int c = lo; c < a.n_chunks; ++c) {
+        const int64_t s0 = a.start_frame[c];
+        if (s0 > f) break;
+        const int i = (int)(f - s0);
+        if (i >= a.K) continue;
+        const float* row = a.scores + ((int64_t)c * a.K + i) * a.n_classes;
+        float m = row[0];
+        for (int k = 1; k < a.n_classes; ++k) {
+            const float v = row[k];
+            m = (m != m || v != v) ? __builtin_nanf("") : fmaxf(m, v);  // np.max: NaN propagates
+        }
+        if (m == m) {  // mask = 1 - isnan
+            acc = acc + m;
+            cnt = cnt + 1.0f;
+            any = true;
+        }
+    }
+    a.out[f] = any ? acc / fmaxf(cnt, 1e-12f) : a.missing;
+}
+}  // namespace wx
+
 using namespace wx;
 
 namespace {
@@ -2522,6 +2574,20 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, cons
 }
 
 }  // extern "C"
+
+extern "C" int wx_vad_aggregate(const float* scores, const int64_t* start_frame, int32_t n_chunks,
+                                int32_t frames_per_chunk, int32_t n_classes, int64_t n_frames, float missing,
+                                float* out, void* stream) {
+    if (n_chunks < 0 || frames_per_chunk < 1 || n_classes < 1 || n_frames < 0) return WX_E_INVALID;
+    if (n_frames == 0) return WX_OK;
+    if (!out || (n_chunks > 0 && (!scores || !start_frame))) return WX_E_INVALID;
+    VadAggArgs a;
+    a.scores = scores; a.start_frame = start_frame; a.n_chunks = n_chunks; a.K = frames_per_chunk;
+    a.n_classes = n_classes; a.n_frames = n_frames; a.missing = missing; a.out = out;
+    const unsigned blocks = (unsigned)((n_frames + 255) / 256);
+    hipLaunchKernelGGL(vad_aggregate_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
 
 #ifdef WX_PHASE_TIMING
 extern "C" int wx_debug_phases(unsigned long long* host, int n) {

@@ -16,6 +16,7 @@ from __future__ import annotations
 from typing import Optional
 
 import numpy as np
+import torch
 
 from . import _lib
 
@@ -154,18 +155,23 @@ class Binarize:
         self.max_duration = max_duration
 
     def regions(self, scores):
-        """GPU state machine: [(starts, ends)] per class column (float64 arrays)."""
-        data = np.asarray(scores.data, dtype=np.float32)
-        if data.ndim == 1:
-            data = data[:, None]
+        """GPU state machine: [(starts, ends)] per class column (float64 arrays).  Scores may
+        be a device tensor (the VAD producer's output): they are then read in place."""
+        data = scores.data
+        if torch.is_tensor(data) and data.is_cuda:
+            data = data.reshape(data.shape[0], -1) if data.dim() > 1 else data[:, None]
+            cols = [data[:, k].contiguous() for k in range(data.shape[1])]
+        else:
+            data = np.asarray(data, dtype=np.float32)
+            if data.ndim == 1:
+                data = data[:, None]
+            cols = [np.ascontiguousarray(data[:, k]) for k in range(data.shape[1])]
         sw = scores.sliding_window
-        cols = [np.ascontiguousarray(data[:, k]) for k in range(data.shape[1])]
         geom = [(float(sw.start), float(sw.step), float(sw.duration))] * len(cols)
         return _lib.binarize(cols, geom, self.onset, self.offset, self.max_duration, self.pad_onset,
                              self.pad_offset)
 
     def __call__(self, scores) -> "Annotation":
-        num_frames, num_classes = np.asarray(scores.data).reshape(len(scores.data), -1).shape
         active = Annotation()
         for k, (rs, re) in enumerate(self.regions(scores)):
             label = k if scores.labels is None else scores.labels[k]
