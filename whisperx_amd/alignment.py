@@ -34,7 +34,7 @@ from typing import Callable, Iterable, List, Optional, Union
 import numpy as np
 import torch
 
-from . import _lib, emission
+from . import _lib, emission, punkt
 from .audio import SAMPLE_RATE, load_audio
 from .types import AlignedTranscriptionResult, SingleAlignedSegment, SingleSegment, SingleWordSegment
 from .utils import interpolate_nans
@@ -161,8 +161,8 @@ def _sentence_spans(text: str):
             _punkt = False
     if _punkt:
         return list(_punkt.span_tokenize(text))
-    # nltk absent: single-sentence span (NLTK's final slice for one sentence)
-    return [(0, len(text.rstrip()))]
+    # nltk absent: the restated untrained-Punkt splitter (parity unpinned, whisperx_amd/punkt.py)
+    return punkt.span_tokenize(text, PUNKT_ABBREVIATIONS)
 
 
 # ------------------------------------------------------------------------------- align()
