@@ -101,12 +101,14 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
  * (3 (N + 1) floats > ~84 KB, i.e. N > ~7000 such tokens) is the segment reported
  * 2 (too many columns) or 3 (hand-off lost) and left uncomputed.
  * min_N/max_N/sum_T describe the batch (host values).
- * Split launches hand halo cells between CUs through a hand-off region of tagged granules
- * and per-segment arrival counters.  wx_align_dp / wx_align_dp_mode carve it out of the
- * workspace and zero it on the stream before the launch (hipMemsetAsync);
- * wx_align_dp_ex takes a separate, caller-owned region instead, which must be all zero
- * before its first use: every launch leaves it all zero again, so no per-launch memset is
- * needed.  One hand-off region must not be used by two launches that may run at the same
+ * Split launches hand halo cells between CUs through a hand-off region of granules tagged
+ * with the launch's 32-bit epoch, plus per-segment arrival counters.  wx_align_dp /
+ * wx_align_dp_mode carve it out of the workspace and zero it on the stream before the launch
+ * (hipMemsetAsync: the workspace may hold anything); wx_align_dp_ex takes a separate,
+ * caller-owned region instead, which must be all zero before its first use and must hold
+ * nothing but hand-off data afterwards: launches leave only their own granules (an older
+ * launch's epoch never matches a later one) and reset the counters, so no per-launch memset
+ * is needed.  One hand-off region must not be used by two launches that may run at the same
  * time (e.g. on two streams). */
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N);
 int wx_align_dp(const float* em, const int64_t* em_off, int32_t V,

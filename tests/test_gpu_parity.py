@@ -226,20 +226,26 @@ def test_align_dp_lost_handoff_recovered(monkeypatch):
     _check_vs_oracle(cases, "after recovery", -1)
 
 
-def test_align_dp_handoff_region_left_zeroed():
-    """wx_align_dp_ex: a split launch leaves its caller-owned hand-off region all zero (the
-    contract that lets callers skip a per-launch memset), and foreign data in a fresh
-    workspace-carved region cannot leak into results (wx_align_dp_mode zeroes it)."""
+def test_align_dp_handoff_region_reuse():
+    """wx_align_dp_ex: one caller-owned hand-off region reused across launches of different
+    batch layouts (granules of earlier launches stay behind in other slots: their epochs
+    never match) gives oracle results every time, and its arrival counters are left at zero;
+    and foreign data in a workspace-carved region (wx_align_dp_mode) is zeroed first."""
     from whisperx_amd import _lib
 
     rng = np.random.default_rng(13)
     cases = _random_cases(rng, 16, (1400, 1600), (300, 500), 32)
+    other = _random_cases(rng, 9, (700, 2600), (200, 700), 32)
+    for c in (cases, other, cases[3:], other, cases):
+        _check_vs_oracle(c, "handoff reuse", 14)
     b = _batch(cases)
     plan = _lib.AlignPlan(b, mode=14)
     for _ in range(3):
         plan.run()
     torch.cuda.synchronize()
-    assert int(plan.ho.count_nonzero()) == 0
+    xg = plan.hob - (b.S + 1) * 4
+    arrive = plan.ho[plan.hob - ((b.S + 1) * 4 + 255) // 256 * 256:].view(torch.int32)[: b.S]
+    assert int(arrive.count_nonzero()) == 0 and xg > 0
     # a workspace full of tag-like garbage through the memset path
     lib = _lib.load()
     wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)

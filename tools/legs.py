@@ -1,0 +1,61 @@
+"""One bench leg in isolation, for rocprofv3 runs (development tool): the program after
+`rocprofv3 ... --` runs exactly this leg's kernel K times after W warm-ups.
+
+    python tools/legs.py cfg2|sat3000|trellis3000 [--steps K] [--warmup W]
+
+cfg2: the headline step (64 x T=1499, V=32, wx_align_dp in the default shape);
+sat3000: 2048 x T=2999, V=32, N~U[850,951], wx_align_dp (throughput shape);
+trellis3000: get_trellis materialised (wx_trellis) on the sat3000 batch."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    import torch
+
+    from satbench import make_batch
+    from whisperx_amd import _lib
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("leg")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    if a.leg == "cfg2":
+        ems, toks = make_batch(64, 1499, 32, 300, 500, 1000, dev)
+    else:
+        ems, toks = make_batch(2048, 2999, 32, 850, 951, 78, dev)
+    b = _lib.Batch(ems, toks, [0] * len(ems), device=dev)
+    del ems
+    if a.leg == "trellis3000":
+        flat, offs = _lib.trellis(b)
+        offs_d = _lib._dev_i64(offs, dev)
+        lib = _lib.load()
+
+        def run():
+            _lib._check(lib.wx_trellis(_lib._ptr(b.em), _lib._ptr(b.em_off_d), b.V, _lib._ptr(b.tok),
+                                       _lib._ptr(b.tok_off_d), _lib._ptr(b.blank), b.S, b.max_N, _lib._ptr(flat),
+                                       _lib._ptr(offs_d), _lib._stream(dev)))
+    else:
+        plan = _lib.AlignPlan(b)
+        run = plan.run
+    for _ in range(a.warmup):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"{a.leg}: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, {b.S} segments", flush=True)
+
+
+if __name__ == "__main__":
+    main()

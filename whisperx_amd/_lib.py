@@ -151,9 +151,10 @@ _ws = Workspace()
 
 
 class Handoff:
-    """Zero-initialised hand-off regions of split launches (wx_align_dp_ex), one per (device,
-    stream): every launch leaves its region all zero, so it is zeroed only when allocated or
-    grown; two streams never share one (concurrent launches must not)."""
+    """Hand-off regions of split launches (wx_align_dp_ex), one per (device, stream): zeroed
+    when allocated or grown, then holding only hand-off granules (a launch never matches an
+    earlier launch's epoch), so no per-launch memset; two streams never share one
+    (concurrent launches must not)."""
 
     def __init__(self):
         self.buf: dict = {}
@@ -294,8 +295,8 @@ class AlignPlan:
         self.status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
         self.wsb = self.lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
         self.ws = torch.empty(max(self.wsb, 1), dtype=torch.uint8, device=dev)
-        # the plan's own hand-off region (zeroed once; its launches keep it zeroed); runs of
-        # one plan are serialised by the caller (one stream at a time)
+        # the plan's own hand-off region (zeroed once; it then holds only hand-off granules);
+        # runs of one plan are serialised by the caller (one stream at a time)
         self.hob = self.lib.wx_align_dp_handoff_bytes(b.S, b.sum_T) if hasattr(self.lib, "wx_align_dp_handoff_bytes") else 1
         self.ho = torch.zeros(max(self.hob, 1), dtype=torch.uint8, device=dev)
         self.args = (_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d), _ptr(b.blank), b.S,

@@ -348,8 +348,10 @@ __device__ unsigned long long wx_loop[8192 * 16 * 3];
 // workgroups ("parts", one per CU), continuing the chunk halo across CUs.  Virtual wave
 // vw = part * W + wv; the first HL lanes of a part's wave 0 mirror the last HL lanes of
 // the previous part's wave W-1, handed over once per 32-row chunk through global memory
-// as 8-byte {value, tag} granules (one sc1 store each; the tag carries the launch epoch and
-// the chunk, so a granule is valid on its own — no flag, no fence).  A part lags its
+// as 8-byte {value, tag} granules (one sc1 store each; the tag is the launch's 32-bit epoch and
+// each chunk has its own slot, so a granule is valid on its own — no flag, no fence; the
+// region is zeroed before first use and holds only granules, so a stale word carries an older
+// launch's epoch and never matches).  A part lags its
 // predecessor by a few chunks; the consumer prefetches each chunk's granules two chunks
 // ahead.  Each part then arrives at a per-segment counter;
 // the last to arrive runs the argmax, the walk and merge_repeats.
@@ -368,7 +370,7 @@ constexpr int kXSlack = WX_XSLACK;  // chunks a part re-builds its lag to (A/B: 
 struct Split {
     int p, P;         // this part, parts per segment
     int lanes;        // bitmap word stride: 64 * W * P
-    unsigned tag;     // epoch << 12 (the chunk index goes in the low 12 bits)
+    unsigned tag;     // the launch epoch (32 bits, never 0)
     uint64_t* xin;    // granules from part p-1: [chunk][kHaloCells] (p > 0)
     uint64_t* xout;   // granules to part p+1 (p < P-1)
     int xstride;      // granules per chunk block of one segment boundary
@@ -439,7 +441,7 @@ struct Forward {
     __device__ __forceinline__ static bool xwait(const uint64_t* xin, int xstride, int q, int l, unsigned tag,
                                                  uint64_t (&xpre)[C], bool& lost, int spin) {
         constexpr int HL = Geometry<C, 2>::HL;
-        const unsigned want = tag | (unsigned)(q & 0xFFF);
+        const unsigned want = tag;  // the slot already encodes the chunk; the tag is the launch
         const uint64_t* gi = xin + (int64_t)q * xstride + min(l, HL - 1) * C;  // all lanes load
         bool ok = true;
 #pragma unroll
@@ -590,7 +592,7 @@ struct Forward {
             if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
                 uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
 #pragma unroll
-                for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag | (unsigned)(q & 0xFFF));
+                for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
             }
             WX_T(c1);
             if (!H) wait_vm();  // this wave's staging (with a helper, DP waves stage nothing)
@@ -1455,15 +1457,6 @@ __device__ unsigned split_arrive(unsigned* c, unsigned epoch, bool lost) {
 }
 
 
-// Zero a split segment's hand-off granules (nch chunk blocks of `stride` granules) with the
-// threads [first_thread, blockDim): a launch leaves its hand-off region as it found it, all
-// zero, so no stale or foreign word can ever carry a valid tag (include/wx_align.h).
-__device__ __forceinline__ void clear_handoff(uint64_t* xseg, int nch, int stride, int first_thread = 0) {
-    const int n = (int)blockDim.x - first_thread;
-    const int64_t total = (int64_t)nch * stride;
-    for (int64_t i = (int)threadIdx.x - first_thread; i < total; i += n) xseg[i] = 0ull;
-}
-
 // Latency buckets (H) claim more than half of a CU's 160 KB LDS so that the dispatcher
 // places one workgroup per CU: two 8-wave workgroups on one CU would share its SIMDs
 // (4 waves per SIMD) while other CUs idle.
@@ -1535,15 +1528,14 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     WX_STAMP_RT(4);
     WX_STAMP(0);
     Split sp;
-    uint64_t* xseg = nullptr;  // SP: this segment's granule block
     if (SP) {
         sp.p = part;
         sp.P = P;
         sp.lanes = kWave * W * P;
-        sp.tag = a.epoch << 12;
+        sp.tag = a.epoch;
         sp.xstride = (kMaxParts - 1) * kHaloCells;
         sp.spin = a.spin;
-        xseg = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
+        uint64_t* xseg = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
         sp.xin = xseg + (part > 0 ? part - 1 : 0) * kHaloCells;
         sp.xout = xseg + part * kHaloCells;
     }
@@ -1589,7 +1581,6 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
                 a.t_start[seg] = 0;
                 a.status[seg] = slow ? 2 : 3;  // (N too large for the generic forward's LDS rows)
             }
-            if (SP) clear_handoff(xseg, (d.T + kChunk - 1) / kChunk, (kMaxParts - 1) * kHaloCells);
             return;
         }
         wait_vm();
@@ -1629,8 +1620,6 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 #endif
     } else {
         if (H && !slow && !failed) fill_q0(E, a.V, d.T, q0, kWave);
-        // the segment's hand-off granules are consumed: zero them for the next launch
-        if (SP && !slow) clear_handoff(xseg, (d.T + kChunk - 1) / kChunk, (kMaxParts - 1) * kHaloCells, kWave);
     }
     wait_vm();
     block_fence();
@@ -2358,7 +2347,7 @@ int split_parts(int32_t S, int mode, int32_t requested) {
 
 unsigned next_epoch() {  // never 0: a zeroed granule or counter carries no valid tag
     static std::atomic<unsigned> e{(unsigned)std::chrono::steady_clock::now().time_since_epoch().count()};
-    const unsigned v = (e.fetch_add(1) + 1) & 0xFFFFFu;
+    const unsigned v = e.fetch_add(1) + 1;
     return v ? v : 1u;
 }
 
