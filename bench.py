@@ -387,6 +387,7 @@ def cpu_align_baseline(threads, budget_s=20.0, seed=11):
             _, ph = _cpu_reference_align(segs, model, synthetic.w2v_dictionary(), audio)
             tot = [a + b for a, b in zip(tot, ph)]
             n += 1
+            log(f"bench: cpu align clip {n} ({threads} threads): {sum(ph):.2f} s")
     finally:
         torch.set_num_threads(old)
     el = sum(tot)
@@ -507,10 +508,12 @@ def main():
     step_s = _allreduce([step_s], "max")[0] if dist_on else step_s
     audio_per_step = float(sum(batch.Ts)) * FRAME_S * world  # seconds of audio aligned per step, all ranks
     value = audio_per_step / step_s
+    log(f"bench[{rank}]: headline {step_s * 1e3:.4f} ms/step")
     corpus = None
     if not args.no_corpus:
         try:
             corpus = corpus_config4(device, rank, world, dist_on)
+            log(f"bench[{rank}]: config4 {corpus['wall_s']:.1f} s")
         except Exception as e:  # never let the secondary leg hide the primary line
             corpus = {"error": repr(e)[:300]}
 
@@ -561,6 +564,7 @@ def main():
             p2 = _lib.AlignPlan(b2)
             h2, d2 = time_steps(p2, 5, 2, False)
             B2 = algorithmic_bytes(b2.Ts, b2.Ns, V)
+            log("bench: saturated T=1499 done")
             extra["saturated"] = {"segments": n_big, "ms_per_step": 1000 * d2 / 5,
                                   "audio_sec_per_s": sum(b2.Ts) * FRAME_S / (d2 / 5),
                                   "achieved_GBps": B2 / (d2 / 5) / 1e9,
@@ -577,6 +581,7 @@ def main():
             p3 = _lib.AlignPlan(b3)
             h3, d3 = time_steps(p3, 3, 1, False)
             B3 = algorithmic_bytes(b3.Ts, b3.Ns, V)
+            log("bench: saturated T=3000 done")
             extra["saturated_T3000"] = {"segments": n3, "ms_per_step": 1000 * d3 / 3,
                                         "audio_sec_per_s": sum(b3.Ts) * FRAME_S / (d3 / 3),
                                         "achieved_GBps": B3 / (d3 / 3) / 1e9,
@@ -615,6 +620,7 @@ def main():
             torch.cuda.empty_cache()
         if not args.no_cpu and world == 1:
             ems_cpu = [e.cpu() for e in ems]
+            log("bench: cpu baselines ...")
             out["cpu_baseline"] = cpu_port_baseline(ems_cpu, toks)
             extra["cpu_c_oracle"] = c_oracle_baseline([e.numpy() for e in ems_cpu], toks)
             extra["host_cpu"] = {"os_cpu_count": os.cpu_count(), "usable_threads": _host_threads(),
@@ -631,6 +637,7 @@ def main():
             except Exception as e:
                 extra["cpu_align_config1"] = {"error": repr(e)[:300]}
         if not args.no_e2e and world == 1:
+            log("bench: e2e legs ...")
             try:
                 extra["e2e_align"] = e2e_align(device)
             except Exception as e:  # never let the secondary leg hide the primary line
@@ -643,6 +650,7 @@ def main():
                 extra["e2e_config3_1h"] = e2e_config3(device)
             except Exception as e:
                 extra["e2e_config3_1h"] = {"error": repr(e)[:200]}
+            log("bench: emission-path MAE ...")
             try:
                 me = mae_e2e(device)
                 out["mae_e2e_ms"] = me["mae_ms"]

@@ -13,6 +13,8 @@
  *                        materialised; a 1-bit decision map replaces it for the backtrack.
  *   wx_binarize       <- whisperx/vad.py:118  Binarize.__call__ (hysteresis + min-cut),
  *                        the kernel under vad.py:264 merge_chunks
+ *   wx_channel_norm   <- whisperx/alignment.py:226-233 (wav2vec2 forward: feature encoder's
+ *                        GroupNorm + GELU, time-major)
  *   wx_vad_aggregate  <- whisperx/vad.py:198-240 VoiceActivitySegmentation.apply's
  *                        segmentation overlap-add (pyannote Inference.aggregate)
  *
@@ -174,6 +176,15 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files,
                 float onset, float offset, double max_duration, double pad_onset, double pad_offset,
                 double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
                 void* stream);
+
+/* Emission producer (alignment.py:226-233, the wav2vec2 forward): GroupNorm with one group
+ * per channel (the first feature-encoder layer) over time-major activations x [L, C] (C % 4
+ * == 0, 16-byte aligned), with the affine gamma/beta (may be NULL) and, when gelu != 0, the
+ * exact erf GELU fused: y = gelu((x - mean_c) / sqrt(var_c + eps) * gamma_c + beta_c).
+ * Statistics in fp64 (biased variance).  y may alias x.  Workspace: see the query. */
+size_t wx_channel_norm_workspace_bytes(int32_t C);
+int wx_channel_norm(const float* x, int64_t L, int32_t C, const float* gamma, const float* beta, float eps,
+                    int32_t gelu, float* y, void* workspace, size_t workspace_bytes, void* stream);
 
 /* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
  * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32

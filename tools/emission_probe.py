@@ -40,9 +40,17 @@ def main():
     torch.cuda.synchronize()
     res = {}
     for name, lens in (("miopen", [5.13, 9.71, 12.37, 17.05, 21.9, 26.41, 29.33, 14.2]),
-                       ("gemm", [5.17, 9.73, 12.39, 17.07, 21.93, 26.43, 29.35, 14.23])):
+                       ("gemm", [5.17, 9.73, 12.39, 17.07, 21.93, 26.43, 29.35, 14.23]),
+                       ("gemm+eager", [5.19, 9.75, 12.41, 17.09, 21.95, 26.45, 29.37, 14.25])):
         if name == "gemm":
             emission.prepare_model(gm)
+        if name == "gemm+eager":
+            try:
+                gm.set_attn_implementation("eager")
+            except Exception as e:  # older transformers
+                print("set_attn_implementation failed", repr(e))
+                gm.config._attn_implementation = "eager"
+            print("attn:", gm.config._attn_implementation, flush=True)
         first, second = [], []
         for sec in lens:
             x = base[: int(sec * 16000)][None].to(dev)
@@ -55,7 +63,14 @@ def main():
                      "fixed30_ms": round(min(t30), 2)}
         print(name, res[name], flush=True)
     # GEMM route vs MIOpen on the same input, and vs CPU
+    y_e = fwd(gm, x30).float().cpu()
+    try:
+        gm.set_attn_implementation("sdpa")
+    except Exception:
+        gm.config._attn_implementation = "sdpa"
     y_g = fwd(gm, x30).float().cpu()
+    d = (y_e - y_g).abs()
+    print("eager-vs-sdpa max", float(d.max()), flush=True)
     emission.restore_model(gm)
     y_m = fwd(gm, x30).float().cpu()
     y_c = fwd(model.cpu(), x30.cpu())

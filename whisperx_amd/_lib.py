@@ -18,6 +18,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WX_LIB_PATH") or os.path.join(_HERE, "libwxalign.so")
 SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
+SRC_PATHS = [SRC_PATH, os.path.join(_HERE, "csrc", "wx_emission.hip")]
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 MAX_VOCAB = 16384
@@ -49,6 +50,8 @@ SIGNATURES = {
     "wx_align_dp_ex": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                       _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _sz, _i32, _vp]),
     "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
+    "wx_channel_norm_workspace_bytes": (_sz, [_i32]),
+    "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
@@ -64,7 +67,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= _newest_source():
         return LIB_PATH
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", f"-I{INCLUDE_DIR}", "-o", LIB_PATH + ".tmp", SRC_PATH]
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", f"-I{INCLUDE_DIR}", "-o", LIB_PATH + ".tmp", *SRC_PATHS]
     res = subprocess.run(cmd, capture_output=not verbose, text=True)
     if res.returncode != 0:
         raise WXError(f"hipcc failed ({res.returncode}):\n{res.stderr}")
@@ -73,7 +76,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def _newest_source() -> float:
-    paths = [SRC_PATH, os.path.join(INCLUDE_DIR, "wx_align.h")]
+    paths = SRC_PATHS + [os.path.join(INCLUDE_DIR, "wx_align.h")]
     return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
 
 
@@ -430,3 +433,30 @@ def vad_aggregate(scores: torch.Tensor, start_frames, n_frames: int, missing: fl
         _check(lib.wx_vad_aggregate(_ptr(sc), _ptr(sf), n_chunks, K, n_cls, int(n_frames), float(missing),
                                     _ptr(out), _stream(dev)))
     return out[: int(n_frames)]
+
+
+def channel_norm(x: torch.Tensor, gamma, beta, eps: float, gelu: bool, out: Optional[torch.Tensor] = None):
+    """wx_channel_norm on a time-major [L, C] fp32 device tensor (contiguous)."""
+    lib = load()
+    L, C = (int(v) for v in x.shape)
+    y = out if out is not None else torch.empty_like(x)
+    wsb = lib.wx_channel_norm_workspace_bytes(C)
+    stream = torch.cuda.current_stream(x.device)
+    # one scratch per (device, stream): align() runs forwards on several streams at once
+    ws = _ws_emit.get(f"{x.device}/{stream.cuda_stream}", wsb, x.device)
+    with torch.cuda.device(x.device):
+        _check(lib.wx_channel_norm(_ptr(x), L, C, _ptr(gamma), _ptr(beta), float(eps), int(bool(gelu)), _ptr(y),
+                                   _ptr(ws), ws.numel(), ctypes.c_void_p(stream.cuda_stream)))
+    return y
+
+
+class _StreamWorkspace(Workspace):
+    def get(self, key, nbytes: int, device=None) -> torch.Tensor:
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_ws_emit = _StreamWorkspace()

@@ -23,11 +23,16 @@ PyTorch-ROCm model call, one per segment, but:
   Parameters are read from the module on every call (``conv.weight`` re-evaluates a
   weight_norm parametrisation), so the module's state_dict and training behaviour are
   untouched; only inference forwards on a HIP device take the GEMM route.
+* **Time-major GroupNorm + GELU.**  The first feature-encoder layer's GroupNorm (one group
+  per channel, i.e. a per-channel normalisation over time) runs as the HIP kernel
+  wx_channel_norm on the time-major conv output with the erf GELU fused, instead of torch's
+  channel-major GroupNorm (which first copied the 96k x 512 activation).
 * **No concatenation copy.**  ``log_softmax`` writes each segment's ``[T, V]`` rows straight
   into its slice of the CSR emission matrix the DP kernel reads (``emissions_csr``).
 """
 from __future__ import annotations
 
+import os
 import types
 from typing import List, Optional, Sequence
 
@@ -107,6 +112,30 @@ def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
     return out.transpose(1, 2)
 
 
+def _is_erf_gelu(act) -> bool:
+    if isinstance(act, torch.nn.GELU):
+        return act.approximate == "none"
+    inner = getattr(act, "act", None)  # transformers' GELUActivation wraps F.gelu
+    return type(act).__name__ == "GELUActivation" and inner is F.gelu
+
+
+def _patched_gn_layer(self, x):
+    """conv -> GroupNorm(one group per channel) -> activation (HF Wav2Vec2GroupNormConvLayer,
+    the feature encoder's first layer) on time-major activations: the GEMM conv, then
+    wx_channel_norm with the erf GELU fused (one HBM read for statistics, one read + write)."""
+    if not (x.is_cuda and not torch.is_grad_enabled() and x.dim() == 3):
+        return self._wx_orig_forward(x)
+    from . import _lib
+
+    gn = self.layer_norm
+    y = _conv1d_gemm(self.conv, x).transpose(1, 2)  # [B, L, C] contiguous (time-major)
+    gelu = _is_erf_gelu(self.activation)
+    for b in range(y.shape[0]):
+        _lib.channel_norm(y[b], gn.weight, gn.bias, gn.eps, gelu, out=y[b])
+    out = y.transpose(1, 2)
+    return out if gelu else self.activation(out)
+
+
 def _patched_forward(self, x):
     if (x.is_cuda and not torch.is_grad_enabled() and x.dim() == 3 and self.padding_mode == "zeros"
             and self.dilation == (1,) and not isinstance(self.padding, str)):
@@ -123,6 +152,12 @@ def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
         if isinstance(mod, torch.nn.Conv1d) and not hasattr(mod, "_wx_orig_forward"):
             mod._wx_orig_forward = mod.forward
             mod.forward = types.MethodType(_patched_forward, mod)
+        gn = getattr(mod, "layer_norm", None)
+        if (not os.environ.get("WX_NO_CHANNEL_NORM") and isinstance(getattr(mod, "conv", None), torch.nn.Conv1d) and isinstance(gn, torch.nn.GroupNorm)
+                and gn.num_groups == gn.num_channels and gn.num_channels % 4 == 0 and hasattr(mod, "activation")
+                and not hasattr(mod, "_wx_orig_forward")):
+            mod._wx_orig_forward = mod.forward
+            mod.forward = types.MethodType(_patched_gn_layer, mod)
     try:
         model._wx_gemm_conv = True
     except Exception:
