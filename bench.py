@@ -78,28 +78,36 @@ def pmc_traffic(kernel):
 
 
 def time_steps(plan, steps, warmup, dist_on):
+    """W untimed warm-up steps, then exactly K steps between two barriers + synchronize; the
+    device time comes from one event pair around the K steps (no per-step event commands
+    between the launches).  A separate, untimed pass with an event pair around every launch
+    gives the kernel's mean duration for the roofline (time_steps.last_launch_s)."""
     for _ in range(warmup):
         plan.run()
     torch.cuda.synchronize()
-    if dist_on:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
-    # one event pair around every step on the stream the kernel runs on (a config-2 batch
-    # maps to one bucket, which wx_align_dp launches directly on the caller's stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    t0 = time.perf_counter()
+    # per-launch kernel time (roofline leg): events on the stream the kernel runs on
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(min(steps, 20))]
     for a, b in ev:
         a.record(stream)
         plan.run()
         b.record(stream)
     torch.cuda.synchronize()
+    time_steps.last_launch_s = float(np.mean([a.elapsed_time(b) / 1000.0 for a, b in ev]))
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        plan.run()
+    e1.record(stream)
+    torch.cuda.synchronize()
     if dist_on:
         torch.distributed.barrier()
     host_s = time.perf_counter() - t0
-    launch_s = [a.elapsed_time(b) / 1000.0 for a, b in ev]
-    dev_s = ev[0][0].elapsed_time(ev[-1][1]) / 1000.0
-    time_steps.last_launch_s = float(np.mean(launch_s))
+    dev_s = e0.elapsed_time(e1) / 1000.0
     return host_s, dev_s
 
 

@@ -848,14 +848,36 @@ struct Forward {
 #pragma unroll
         for (int k = 0; k < C; ++k) ga[k] = bb + toff[k];
         Row rw[kChunk];
-        load_row<COL>(bb, ga, 0, boff, c0q, rw[0]);
-        load_row<COL>(bb, ga, kRowBytes, boff, c0q + 1, rw[1]);
+        // COL 3 (column 0 from the helper's LDS row): the chunk's 32 values in 8 16-byte
+        // loads up front instead of an address move + ds_read_b32 per step in the wave that
+        // paces the chain (the column-1 wave)
+        float c0r[COL == 3 ? kChunk : 1];
+        if constexpr (COL == 3) {
+#pragma unroll
+            for (int i = 0; i < kChunk / 4; ++i) {
+                const float4 v = reinterpret_cast<const float4*>(c0q)[i];
+                c0r[4 * i] = v.x;
+                c0r[4 * i + 1] = v.y;
+                c0r[4 * i + 2] = v.z;
+                c0r[4 * i + 3] = v.w;
+            }
+        }
+        constexpr int LC = COL == 3 ? 4 : COL;  // load_row without the per-step column-0 read
+        auto c0_of = [&](Row& r, int u) {
+            if constexpr (COL == 3) r.c0 = c0r[u];
+        };
+        load_row<LC>(bb, ga, 0, boff, c0q, rw[0]);
+        load_row<LC>(bb, ga, kRowBytes, boff, c0q + 1, rw[1]);
+        c0_of(rw[0], 0);
+        c0_of(rw[1], 1);
         float hist[kUnroll];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u) {
             if ((u & 1) == 0 && u + 2 < kChunk) {
-                load_row<COL>(bb, ga, (u + 2) * kRowBytes, boff, c0q + u + 2, rw[u + 2]);
-                load_row<COL>(bb, ga, (u + 3) * kRowBytes, boff, c0q + u + 3, rw[u + 3]);
+                load_row<LC>(bb, ga, (u + 2) * kRowBytes, boff, c0q + u + 2, rw[u + 2]);
+                load_row<LC>(bb, ga, (u + 3) * kRowBytes, boff, c0q + u + 3, rw[u + 3]);
+                c0_of(rw[u + 2], u + 2);
+                c0_of(rw[u + 3], u + 3);
             }
             __builtin_amdgcn_sched_barrier(0);
             advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
@@ -1491,7 +1513,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 4 * kChunk * VS ? kLatencyLdsFloats : 4 * kChunk * VS)
                                  : 2 * kChunk * VS;
     __shared__ float lds[kLdsFloats];
-    __shared__ float c0b[H ? 2 * kChunk : 1];
+    __shared__ __attribute__((aligned(16))) float c0b[H ? 2 * kChunk : 1];
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
