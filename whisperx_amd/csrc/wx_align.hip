@@ -1023,6 +1023,64 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
     return uniform(nan_row != 0x7fffffff ? nan_row : best_row);
 }
 
+// column_argmax with every thread of a multi-wave workgroup (all threads must call it):
+// rows strided over the threads, 8 loads in flight each, then a wave reduction and one LDS
+// exchange (red: 3 ints per wave).  Same semantics: first maximum, the first NaN wins.
+__device__ int block_argmax(const float* __restrict__ cn, int T, int* red) {
+    const int tid = (int)threadIdx.x, n = (int)blockDim.x;
+    int nan_row = 0x7fffffff, best_row = 0;
+    float best = -INFINITY;
+    constexpr int kBatch = 8;
+    for (int base = tid; base < T; base += kBatch * n) {
+        float v[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+            const int i = base + u * n;
+            v[u] = i < T ? cn[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {  // this thread's rows in increasing order
+            const int row = base + u * n + 1;
+            if (v[u] != v[u]) {
+                nan_row = min(nan_row, row);
+            } else if (v[u] > best) {
+                best = v[u];
+                best_row = row;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        nan_row = min(nan_row, __shfl_xor(nan_row, off));
+        const float b2 = __shfl_xor(best, off);
+        const int r2 = __shfl_xor(best_row, off);
+        if (b2 > best || (b2 == best && r2 < best_row)) {
+            best = b2;
+            best_row = r2;
+        }
+    }
+    const int w = tid >> 6, nw = (n + kWave - 1) / kWave;
+    if ((tid & (kWave - 1)) == 0) {
+        red[3 * w] = nan_row;
+        red[3 * w + 1] = __builtin_bit_cast(int, best);
+        red[3 * w + 2] = best_row;
+    }
+    __syncthreads();
+    nan_row = red[0];
+    best = __builtin_bit_cast(float, red[1]);
+    best_row = red[2];
+    for (int k = 1; k < nw; ++k) {
+        nan_row = min(nan_row, red[3 * k]);
+        const float b2 = __builtin_bit_cast(float, red[3 * k + 1]);
+        const int r2 = red[3 * k + 2];
+        if (b2 > best || (b2 == best && r2 < best_row)) {
+            best = b2;
+            best_row = r2;
+        }
+    }
+    return uniform(nan_row != 0x7fffffff ? nan_row : best_row);
+}
+
 // ------------------------------------------------------------------------------------
 // Generic forward of one segment by the whole workgroup: one time step per barrier, cells
 // strided over the threads, rows ping-ponged in LDS.  Orders of magnitude slower than
@@ -1517,6 +1575,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
+    __shared__ int argred[3 * (W + H)];
     __shared__ ColMapLds<VS> cml;
     const int P = SP ? a.parts : 1;
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
@@ -1612,8 +1671,10 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 #ifdef WX_PHASE_TIMING
     WX_T(w0);
 #endif
+    // t_start: with every wave when the workgroup has several (the walk waits for it)
+    const int ts_block = (W + H > 1) ? block_argmax(cn, d.T, argred) : 0;
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
-        const int ts = column_argmax(cn, d.T);
+        const int ts = (W + H > 1) ? ts_block : column_argmax(cn, d.T);
 #ifdef WX_PHASE_TIMING
         WX_T(w1);
 #endif
