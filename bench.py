@@ -245,7 +245,7 @@ def e2e_config3(device, seed=3):
                     "synthetic scores/audio/transcripts"}
 
 
-def vad_producer_1h(device, seed=5, batch_size=128):
+def vad_producer_1h(device, seed=5, batch_size=2048):
     """VAD producer (vad.py:198-240) on 1 h of audio: 7,191 five-second windows every 0.5 s
     through the random-weight PyanNet-shaped segmentation model (batched) and the overlap-add
     HIP kernel.  Timing only (random weights: merge_chunks over these scores is exercised by

@@ -94,10 +94,13 @@ def closest_frame(t: float, start: float, duration: float, step: float) -> int:
 class VoiceActivitySegmentation:
     """vad.py:198-240: speech scores of a waveform as a SlidingWindowFeature [frames, 1] whose
     data stays a device tensor.  ``duration``/``step`` are the sliding windows (5 s / 0.5 s),
-    ``batch_size`` the windows per model forward (pyannote's default 32)."""
+    ``batch_size`` the windows per model forward.  pyannote's default is 32; the forward is
+    host-bound at that size (MIOpen's LSTM costs ~25 ms of host time per call), so the
+    default here is 1024 windows (~2.6 GB of activations; 1 h: 2.2 s at 128, 1.15 s at 2048 on
+    MI355X; MIOpen's LSTM rejects batches of ~7,000)."""
 
     def __init__(self, segmentation: Optional[torch.nn.Module] = None, device="cuda", duration: float = 5.0,
-                 step: Optional[float] = None, batch_size: int = 32):
+                 step: Optional[float] = None, batch_size: int = 1024):
         self.device = torch.device(device)
         self.model = (segmentation if segmentation is not None else PyanNet()).to(self.device).eval()
         self.duration = float(duration)
