@@ -19,9 +19,8 @@ the fp32 sums are the reference's sequential ones).  The scores stay on the devi
 ``Binarize``/``merge_chunks`` read them in place (``wx_binarize``).
 
 The whisperX VAD checkpoint (``VAD_SEGMENTATION_URL``) cannot be fetched offline: ``PyanNet``
-builds the architecture with random weights, which is what the benchmarks time, and loads a
-state_dict when given one (``load_state_dict`` / ``from_checkpoint`` with ``torch.load(...,
-weights_only=True)``).  Parity of the aggregation is pinned to a restatement of pyannote's
+builds the architecture with random weights, which is what the benchmarks time; a state_dict
+loads with ``load_state_dict`` (read the file with ``torch.load(..., weights_only=True)``).  Parity of the aggregation is pinned to a restatement of pyannote's
 published algorithm (oracle.vad_aggregate), not to pyannote itself, which is absent:
 "parity unpinned" at the pyannote boundary.
 """
