@@ -406,7 +406,7 @@ struct Geometry {
     }
 };
 
-template <int C, int VS, int MODE, int W, bool H, bool SP = false>
+template <int C, int VS, int MODE, int W, bool H, bool SP = false, int NH = 1>
 struct Forward {
     static constexpr int kRowBytes = VS * 4;
     static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves; SP: Split::lanes)
@@ -478,8 +478,11 @@ struct Forward {
         const int lanes = SP ? sp->lanes : kLanes;
         const int T = d.T, N = d.N;
         const int nch = (T + kChunk - 1) / kChunk;
-        if (H && wv == W) {
-            helper(d, E, V, lds, c0b, nch, x4, cm, !SP || sp->p == 0);
+        if (H && wv >= W) {
+            // NH == 2 (split kernels): wave W stages, wave W + 1 runs column 0's fp64 chain;
+            // one helper doing both paced part 0 (it reached every chunk barrier last)
+            const bool col0 = (!SP || sp->p == 0) && (NH == 1 || wv == W + 1);
+            helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
             return false;
         }
         const int l = lane_id();
@@ -699,7 +702,7 @@ struct Forward {
     // q+1 are staged and column 0 of chunk q is in c0b[q & 1].  (q0 is filled after the
     // forward pass, while wave 0 walks: fill_q0.)
     __device__ static void helper(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* c0b,
-                                  int nch, bool x4, const ColMap& cm, bool col0) {
+                                  int nch, bool x4, const ColMap& cm, bool col0, bool stage = true) {
         const int T = d.T, N = d.N;
         const int inf_from = T + 1 - N;
         double acc = 0.0;  // sum of em[0..t-1, 0], uniform
@@ -707,17 +710,31 @@ struct Forward {
         // ahead, so each chunk's loads have two chunk times to land: at chunk q only the
         // loads of chunk q+2 may still be in flight (vmcnt = that chunk's instruction
         // count: 4 for 16-byte staging, 32 for row staging; gathers drain fully).
-        for (int i = 0; i < 3 && i < nch; ++i)
-            stage_rows<VS, 1, true>(E, V, i * kChunk, min(kChunk, T - i * kChunk), lds + i * kChunk * VS, x4, cm);
-        wait_vm();
-        if (col0) column0(0, T, inf_from, lds, c0b, acc);
+        if (stage) {
+            for (int i = 0; i < 3 && i < nch; ++i)
+                stage_rows<VS, 1, true>(E, V, i * kChunk, min(kChunk, T - i * kChunk), lds + i * kChunk * VS, x4, cm);
+            wait_vm();
+        }
+        // chunk 0's column 0: from the staged rows, or (a column-only helper, which cannot
+        // know when the other helper's staging landed) straight from the emission rows
+        if (col0) {
+            if (stage) {
+                column0(0, T, inf_from, lds, c0b, acc);
+            } else {  // chunk 0 column 0 into the 4th buffer (first staged after barrier 0)
+                float* own = lds + 3 * kChunk * VS;
+                if (lane_id() < min(kChunk, T)) own[lane_id() * VS] = E[(int64_t)lane_id() * V];
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                column0(0, T, inf_from, own, c0b, acc);
+            }
+        }
 #ifdef WX_PHASE_TIMING
         unsigned long long acc_c0 = 0, acc_bar = 0, acc_other = 0;
 #endif
         for (int q = 0; q < nch; ++q) {
             WX_T(h0);
             // chunk q+1 must have landed; chunk q+2 (staged at q-1) may still be in flight
-            if (q + 2 < nch && T - (q + 2) * kChunk >= kChunk && VS != kGatherVS) {
+            if (!stage) {
+            } else if (q + 2 < nch && T - (q + 2) * kChunk >= kChunk && VS != kGatherVS) {
                 if (x4 && VS == 32)
                     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 else
@@ -728,11 +745,12 @@ struct Forward {
             WX_T(h1);
             __syncthreads();
             WX_T(h2);
-            if (q + 3 < nch)
+            if (stage && q + 3 < nch)
                 stage_rows<VS, 1, true>(E, V, (q + 3) * kChunk, min(kChunk, T - (q + 3) * kChunk),
                                         lds + ((q + 3) % kBufs) * kChunk * VS, x4, cm);
             WX_T(h3);
-            if (col0 && q + 1 < nch) column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
+            if (col0 && q + 1 < nch)
+                column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
             WX_T(h4);
 #ifdef WX_PHASE_TIMING
             acc_c0 += h4 - h3;
@@ -742,7 +760,7 @@ struct Forward {
         }
 #ifdef WX_PHASE_TIMING
         if (lane_id() == 0 && blockIdx.x < 8192) {
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W) * 3;
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W + (stage ? 0 : 1)) * 3;
             o[0] = acc_c0;
             o[1] = acc_bar;
             o[2] = acc_other;
@@ -1588,7 +1606,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if (SP && seg >= a.S) return;  // grid padded to a multiple of 8 segments
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     const int want = (SP || a.parts > 1) ? launch_split_bucket(d.N, a.parts, a.split_id) : bucket_id(d.N, a.mode);
-    if (want != (bucket_make(C, W, H) | (SP ? kSplitFlag : 0))) return;  // another instantiation owns it
+    if (want != (bucket_make(C, W, H ? 1 : 0) | (SP ? kSplitFlag : 0))) return;  // another instantiation owns it
     const int lane = (int)threadIdx.x;
     if (d.N <= 0 || d.T <= 0) {
         if (lane == 0 && part == 0) {
@@ -1623,7 +1641,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if (SP && lane == 0) tsb[2] = 0;
     bool lost = false;
     if (!slow)
-        lost = Forward<C, VS, 0, W, H != 0, SP>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
+        lost = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
                                                      a.x4 != 0, cm, nullptr, &sp);
     WX_STAMP(1);
     if (SP && lost) tsb[2] = 1;  // (any lane of wave 0)
@@ -1724,9 +1742,9 @@ __global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1
 
 // Split segments: P workgroups (parts, one per CU) per segment, grid = ceil(S / 8) * 8 * P.
 template <int C, int VS, int W>
-__global__ __launch_bounds__(kWave*(W + 1)) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
+__global__ __launch_bounds__(kWave*(W + 2)) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
     AlignArgs a) {
-    align_dp_body<C, VS, W, 1, true>(a);
+    align_dp_body<C, VS, W, 2, true>(a);
 }
 
 template <int C, int VS, int W, int H>
@@ -2505,7 +2523,7 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
     return fork_join(st, n, [&](int i, hipStream_t s) {
 #define WX_LAUNCH_SPLIT(CC, WW)                                                                        \
         if (ids[i] == (bucket_make(CC, WW, 1) | kSplitFlag)) {                                          \
-            const dim3 g2(split_grid(S, a.parts)), b2(kWave * (WW + 1));                                 \
+            const dim3 g2(split_grid(S, a.parts)), b2(kWave * (WW + 2));                                 \
             if (V <= 32) hipLaunchKernelGGL((align_dp_split_kernel<CC, 32, WW>), g2, b2, 0, s, a);       \
             else if (V <= 64) hipLaunchKernelGGL((align_dp_split_kernel<CC, 64, WW>), g2, b2, 0, s, a);  \
             else hipLaunchKernelGGL((align_dp_split_kernel<CC, kGatherVS, WW>), g2, b2, 0, s, a);        \
