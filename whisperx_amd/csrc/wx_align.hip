@@ -639,7 +639,7 @@ struct Forward {
                 for (int k = 0; k < C; ++k)
                     xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
             }
-            if (SP && MODE == 0 && q > 0 && !halo) store_deferred(q - 1);
+            if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
@@ -666,7 +666,7 @@ struct Forward {
                     const unsigned wq = (sh == 0) ? st.w[k] : (st.w[k] << sh);
                     if (SP)
                         wdef[k] = wq;
-                    else if (!halo)
+                    else if (!halo && g < L.G)  // (lanes past column N: words the walk never reads)
                         bits[((int64_t)q * C + k) * lanes + g] = wq;
                     st.w[k] = 0u;
                 }
@@ -677,7 +677,7 @@ struct Forward {
                 chunk_iter(q, xeven);
                 if (q + 1 < nch) chunk_iter(q + 1, xodd);
             }
-            if (MODE == 0 && nch > 0 && !halo) store_deferred(nch - 1);
+            if (MODE == 0 && nch > 0 && !halo && g < L.G) store_deferred(nch - 1);
         } else {
             for (int q = 0; q < nch; ++q) chunk_iter(q, xeven);
         }
