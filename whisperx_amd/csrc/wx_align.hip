@@ -2046,6 +2046,11 @@ __device__ __forceinline__ void argmin_combine(float& v, int64_t& f, bool& nan, 
     }
 }
 
+#ifndef WX_SCANQ
+#define WX_SCANQ 2
+#endif
+constexpr int kScanQ = WX_SCANQ;  // frames per lane per event-scan iteration (1 h merge_chunks A/B: 2 -> 7.8 ms, 4 -> 9.4, 8 -> 12.7)
+
 __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
     const int file = blockIdx.x;
     const int lane = lane_id();
@@ -2085,11 +2090,11 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
         // ---- find the next event frame e >= i
         int64_t ev = -1;
         bool split = false;
-        for (int64_t base = i; base < F && ev < 0; base += 4 * kWave) {
-            unsigned long long m[4];
-            unsigned long long ms[4];
+        for (int64_t base = i; base < F && ev < 0; base += kScanQ * kWave) {
+            unsigned long long m[kScanQ];
+            unsigned long long ms[kScanQ];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < kScanQ; ++q) {
                 const int64_t f = base + q * kWave + lane;
                 bool p = false, ps = false;
                 if (f < F) {
@@ -2105,7 +2110,7 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
                 ms[q] = __ballot(ps);
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < kScanQ; ++q) {
                 if (ev < 0 && m[q]) {
                     const int l = __ffsll((long long)m[q]) - 1;
                     ev = base + q * kWave + l;
@@ -2130,9 +2135,18 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
             int64_t bf = -1;
             bool bn = false;
             const int64_t fa = lo + max<int64_t>(sa - (has_stale ? 1 : 0), 0);
-            for (int64_t f = fa + lane; f < ev; f += kWave) {
-                const float v = y[f];
-                argmin_combine(bv, bf, bn, v, f, v != v);
+            for (int64_t f0 = fa + lane; f0 < ev; f0 += 8 * kWave) {  // 8 loads in flight per lane
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t f = f0 + u * kWave;
+                    v[u] = f < ev ? y[f] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {  // this lane's frames in increasing order
+                    const int64_t f = f0 + u * kWave;
+                    if (f < ev) argmin_combine(bv, bf, bn, v[u], f, v[u] != v[u]);
+                }
             }
 #pragma unroll
             for (int off = 1; off < kWave; off <<= 1) {
