@@ -410,13 +410,14 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
                                float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(r_off_d),
                                _ptr(cnt), _stream(dev)))
     cnt_h = cnt.cpu().numpy()
-    rs_h, re_h = rs.cpu().numpy(), re.cpu().numpy()
     out = []
     for i in range(len(F)):
         n = int(cnt_h[i])
         if n < 0:
             raise WXError("binarize region buffer overflow")
-        out.append((rs_h[r_off[i]:r_off[i] + n], re_h[r_off[i]:r_off[i] + n]))
+        # copy back only the regions found (the buffers hold F + 1 slots per column)
+        a = r_off[i]
+        out.append((rs[a:a + n].cpu().numpy(), re[a:a + n].cpu().numpy()))
     return out
 
 
