@@ -63,10 +63,17 @@ def test_config4_corpus_pipeline_full_size_vs_oracle():
             segs = tr.segments(chunks)
             assert all(s["start"] == round(c["start"], 3) and s["end"] == round(c["end"], 3)
                        for s, c in zip(segs, chunks))
+            mark = len(captured)
             out = whisperx_amd.align(segs, model, meta, audio_buf[: int(dur * 16000)], dev)
             n_chunks += len(segs)
             n_words += len(out["word_segments"])
-            ems, toks, blanks, res = captured.pop()
+            # align() runs the DP one group of segments at a time: concatenate this call's groups
+            calls = captured[mark:]
+            del captured[mark:]
+            ems = [e for c in calls for e in c[0]]
+            toks = [t for c in calls for t in c[1]]
+            blanks = [b for c in calls for b in c[2]]
+            res = [r for c in calls for r in c[3]]
             assert len(ems) == len(segs)
             for k in range(0, len(ems), 3):  # every third chunk of every file
                 ok, ts, ss, se, sc = oracle.align_dp(ems[k], toks[k], blanks[k])

@@ -239,12 +239,24 @@ class _EmissionsCSR:
     """Log-probabilities of S segments packed as one [sum_T, V] fp32 device matrix (the DP
     kernel's input layout); iterating yields each segment's [T, V] row slice."""
 
-    def __init__(self, em: torch.Tensor, Ts):
+    def __init__(self, em: torch.Tensor, Ts, events=None):
         self.em = em
         self.Ts = list(Ts)
         self.off = [0]
         for T in self.Ts:
             self.off.append(self.off[-1] + T)
+        self.events = events  # per segment: recorded on its forward's stream after log_softmax
+        self.streams = []
+
+    def sub(self, a: int, b: int) -> "_EmissionsCSR":
+        """Segments [a, b) as their own packed matrix (a row-range view: no copy)."""
+        ev = self.events[a:b] if self.events is not None else None
+        return _EmissionsCSR(self.em[self.off[a]: self.off[b]], self.Ts[a:b], ev)
+
+    def wait(self, stream):
+        """Make `stream` wait for these segments' forwards."""
+        for ev in self.events or ():
+            stream.wait_event(ev)
 
     def __len__(self):
         return len(self.Ts)
@@ -296,9 +308,11 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = 4):
         streams = [torch.cuda.Stream(device=dev) for _ in range(max(n_streams, 1))]
         _EMISSION_STREAMS[key] = streams
     bad = False
+    csr.events = []
+    for st in streams:
+        st.wait_stream(main)
     for i, w in enumerate(waveforms):
         st = streams[i % len(streams)]
-        st.wait_stream(main)
         with torch.cuda.stream(st):
             lg = _logits(model, model_type, w, device)
             if tuple(lg.shape) != (1, Ts[i], V):
@@ -306,10 +320,16 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = 4):
                 break
             with torch.inference_mode():
                 emission.log_softmax_into(lg[0], csr[i])
-    for st in streams:
-        main.wait_stream(st)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            csr.events.append(ev)
     if bad:
+        for st in streams:
+            main.wait_stream(st)
         return [_emission(model, model_type, w, device) for w in waveforms]
+    # not joined here: align() runs the DP group by group as their forwards finish, then
+    # joins every stream back onto the current one
+    csr.streams = streams
     return csr
 
 
@@ -370,6 +390,10 @@ def align(
     # 2a. emissions for every alignable segment, queued on the device
     blank_id = blank_id_of(model_dictionary)
     dp_dev = _dp_device(device)
+    if torch.device(device).type == "cuda" and not audio.is_cuda:
+        # one host->device copy of the waveform: per-segment copies from pageable memory would
+        # each wait for their stream's earlier forwards, keeping the host in lock-step with them
+        audio = audio.to(dp_dev)
     plan = []  # per segment: ("skip", reason) | ("dp", index into batch)
     ems, toks, blanks, meta = [], [], [], []
     for sdx, segment in enumerate(transcript):
@@ -393,14 +417,19 @@ def align(
     with _Phase("emission"):
         ems = _emissions(model, model_type, ems, device)
 
-    # 2b. one fused DP launch for all segments
-    with _Phase("dp"):
-        results = _run_dp(ems, toks, blanks, dp_dev) if len(ems) else []
-
-    # 2c. timestamps and aggregation, in segment order (same prints, same order)
-    with _Phase("aggregate"):
-        aligned_segments = _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method,
-                                          return_char_alignments)
+    # 2b. the fused DP, one launch per group of segments, and 2c. timestamps and aggregation in
+    # segment order (same prints, same order).  A group's DP waits only for its own forwards, so
+    # the host aggregates group g while the GPU still runs the forwards of the later groups.
+    with _Phase("dp+aggregate"):
+        results = _GroupedDP(ems, toks, blanks, dp_dev)
+        try:
+            aligned_segments = _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method,
+                                              return_char_alignments)
+        finally:
+            if isinstance(ems, _EmissionsCSR):
+                main = torch.cuda.current_stream(dp_dev)
+                for st in ems.streams:
+                    main.wait_stream(st)
     word_segments: List[SingleWordSegment] = []
     for segment in aligned_segments:
         word_segments += segment["words"]
@@ -434,8 +463,28 @@ def _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_meth
     return aligned_segments
 
 
+class _GroupedDP:
+    """DP results by segment index, computed one group of segments at a time on first use
+    (each group: one wx_align_dp launch after that group's forwards, one host copy)."""
+
+    def __init__(self, ems, toks, blanks, dev, n_groups: int = 4, min_group: int = 8):
+        self.ems, self.toks, self.blanks, self.dev = ems, toks, blanks, dev
+        n = len(ems)
+        self.size = max(min_group, -(-n // n_groups)) if n else 1
+        self.res = [None] * n
+
+    def __getitem__(self, i):
+        if self.res[i] is None:
+            a = (i // self.size) * self.size
+            b = min(len(self.res), a + self.size)
+            sub = self.ems.sub(a, b) if isinstance(self.ems, _EmissionsCSR) else self.ems[a:b]
+            self.res[a:b] = _run_dp(sub, self.toks[a:b], self.blanks[a:b], self.dev)
+        return self.res[i]
+
+
 def _run_dp(ems, toks, blanks, dev):
     if isinstance(ems, _EmissionsCSR) and ems.em.device == dev:
+        ems.wait(torch.cuda.current_stream(dev))
         batch = _lib.Batch.from_csr(ems.em, ems.Ts, toks, blanks)
     else:
         batch = _lib.Batch(list(ems), toks, blanks, device=dev)
