@@ -280,9 +280,9 @@ def _vocab_size(model, model_type):
 _EMISSION_STREAMS = {}
 
 
-def _emissions(model, model_type, waveforms, device, n_streams: int = 4):
+def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.environ.get("WX_EMISSION_STREAMS", "8"))):
     """Emissions of every segment, one unpadded forward each (padding would change wav2vec2's
-    logits, alignment.py:217-233), issued round-robin on `n_streams` HIP streams: one 30 s
+    logits, alignment.py:217-233), issued round-robin on `n_streams` (8; A/B on config 3: 2 / 4 / 8 streams 803 / 790 / 755 ms) HIP streams: one 30 s
     forward's GEMMs (1,499 rows) fill a fraction of the GPU, so consecutive segments overlap.
     On a HIP device each forward's log_softmax writes straight into its rows of one packed
     [sum_T, V] matrix (returned as _EmissionsCSR), which the DP reads in place; the model's
