@@ -193,7 +193,7 @@ def e2e_align(device, n_seg=16, seed=7):
     return {"value": 30.0 * n_seg / dt, "unit": "audio-sec/s", "segments": n_seg, "words": n_words,
             "ms_per_segment": 1000 * dt / n_seg,
             "note": "align() incl. random-weight wav2vec2-base fp32 forward per segment on the GPU "
-                    "(4 HIP streams, one unpadded forward per segment)"}
+                    "(8 HIP streams, one unpadded forward per segment)"}
 
 
 def e2e_config3(device, seed=3):
