@@ -123,6 +123,44 @@ def test_align_dp_random_mixed_buckets_vs_oracle(V, mode):
     _check_vs_oracle(cases, f"V{V} mode {mode}", mode)
 
 
+def _skewed_cases(rng, V=32):
+    """Segments whose path is far from the straight line the speculative walk guesses from
+    (walk_spec): all tokens in the last or first fifth, bursts, flat noise, exact ties."""
+    cases = []
+    for kind in ("late", "early", "bursts", "flat", "ties"):
+        for _ in range(3):
+            T = int(rng.integers(900, 1500))
+            N = int(rng.integers(150, 420))
+            logits = rng.standard_normal((T, V)).astype(np.float32)
+            toks = rng.integers(1, V, N)
+            if kind == "late":
+                fr = np.sort(rng.choice(np.arange(T - T // 5, T - 1), min(N, T // 5 - 2), replace=False))
+            elif kind == "early":
+                fr = np.sort(rng.choice(np.arange(1, T // 5), min(N, T // 5 - 2), replace=False))
+            elif kind == "bursts":
+                lo = np.concatenate([np.arange(s, s + 60) for s in range(20, T - 80, 240)])
+                fr = np.sort(rng.choice(lo, min(N, len(lo)), replace=False))
+            else:
+                fr = np.sort(rng.choice(np.arange(1, T - 1), N, replace=False))
+            toks = toks[: len(fr)]
+            if kind != "flat":
+                logits[:, 0] += 6.0
+                logits[fr, toks] += 12.0
+            em = torch.log_softmax(torch.from_numpy(logits), -1).numpy()
+            if kind == "ties":
+                em = (np.round(em * 4) / 4).astype(np.float32)
+            cases.append({"em": np.ascontiguousarray(em), "tokens": toks.astype(np.int64), "blank": np.int64(0)})
+    return cases
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_align_dp_speculative_walk_skewed_paths(mode):
+    """The multi-wave kernels walk the backtrack in segments from guessed columns and keep a
+    segment only where the true walk merged with it; paths far from the guess must still
+    equal the oracle's."""
+    _check_vs_oracle(_skewed_cases(np.random.default_rng(7)), f"skewed mode {mode}", mode)
+
+
 def _capacity(C, W):
     """Tokens a (C cells/lane, W waves) bucket holds: waves >= 1 give ceil(32/C) lanes to the
     chunk halo (wx_align.hip, Geometry)."""

@@ -260,6 +260,18 @@ __device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, i
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+__device__ __forceinline__ void wave_fence() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void block_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Column-0 value tr[t][0]: 0 / fp32(cumsum) / +inf in the last N rows (alignment.py:367-370).
 __device__ __forceinline__ float col0_value(int t, double acc, int T, int N) {
     const bool inf_row = (N == 0) || (t >= T + 1 - N);
@@ -1168,10 +1180,13 @@ __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bit
     // Unconditional (column clamped to 1, block to 0): the walk masks invalid lanes when it
     // uses the word, so the load can stay in flight across blocks (a conditional load
     // merges into its destination and hipcc then waits for it where it is issued).
+    // The block's row base is wave-uniform (scalar 64-bit math); the lane adds a 32-bit word
+    // offset, so the load takes the saddr + voffset form with no per-lane 64-bit multiply.
+    const unsigned* row = bits + (int64_t)uniform(max(b, 0)) * (lay.C * lay.lanes);
     const int jj = max(A - lane_id(), 1);
     int g, k;
     lay.locate<CC>(jj - 1, g, k);
-    return bits[((int64_t)max(b, 0) * lay.C + k) * lay.lanes + g];
+    return row[(unsigned)(k * lay.lanes + g)];
 }
 
 // Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d; steps
@@ -1224,33 +1239,36 @@ __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
     // it (lane dd + 1 may be past the window: read, never used).  Unrolled by four: a taken
     // branch costs more than the rest of a change (measured ~96 cycles per change for the
     // loop with one taken branch per change).
-    unsigned cm = 0u, m = 0xFFFFFFFFu, x, wn, t, p;
-    int dd = d;
-#define WX_RL_STEP(BR)                          \
+    // The lane position is not carried through the chain: every change sets one bit of cm, so
+    // the walk leaves the block on lane d + popcount(cm).  Words are read two changes ahead
+    // (wa / wb alternate), which keeps v_readlane's SGPR write two changes off its reader.
+    unsigned cm = 0u, m = 0xFFFFFFFFu, x, wa, wb, t = (unsigned)d + 2u, p;
+#define WX_RL_STEP(W, BR)                       \
     "s_ff1_i32_b32 %[p], %[x]\n\t"              \
     "s_bitset1_b32 %[cm], %[p]\n\t"             \
     "s_lshl_b32 %[m], -2, %[p]\n\t"             \
-    "s_add_u32 %[dd], %[dd], 1\n\t"             \
-    "s_add_u32 %[t], %[dd], 1\n\t"              \
-    "s_and_b32 %[x], %[wn], %[m]\n\t"           \
-    "v_readlane_b32 %[wn], %[win], %[t]\n\t" BR "\n\t"
+    "s_add_u32 %[t], %[t], 1\n\t"               \
+    "s_and_b32 %[x], %[" #W "], %[m]\n\t"       \
+    "v_readlane_b32 %[" #W "], %[win], %[t]\n\t" BR "\n\t"
     asm volatile(
-        "v_readlane_b32 %[x], %[win], %[dd]\n\t"
-        "s_add_u32 %[t], %[dd], 1\n\t"
-        "v_readlane_b32 %[wn], %[win], %[t]\n\t"
+        "s_add_u32 %[p], %[t], -2\n\t"
+        "v_readlane_b32 %[x], %[win], %[p]\n\t"
+        "s_add_u32 %[p], %[t], -1\n\t"
+        "v_readlane_b32 %[wa], %[win], %[p]\n\t"
+        "v_readlane_b32 %[wb], %[win], %[t]\n\t"
         "s_and_b32 %[x], %[x], %[m]\n\t"
         "s_cbranch_scc0 2f\n"
         "1:\n\t"
-        WX_RL_STEP("s_cbranch_scc0 2f")
-        WX_RL_STEP("s_cbranch_scc0 2f")
-        WX_RL_STEP("s_cbranch_scc0 2f")
-        WX_RL_STEP("s_cbranch_scc1 1b")
+        WX_RL_STEP(wa, "s_cbranch_scc0 2f")
+        WX_RL_STEP(wb, "s_cbranch_scc0 2f")
+        WX_RL_STEP(wa, "s_cbranch_scc0 2f")
+        WX_RL_STEP(wb, "s_cbranch_scc1 1b")
         "2:"
-        : [dd] "+s"(dd), [cm] "+s"(cm), [m] "+s"(m), [x] "=&s"(x), [wn] "=&s"(wn), [t] "=&s"(t), [p] "=&s"(p)
+        : [t] "+s"(t), [cm] "+s"(cm), [m] "+s"(m), [x] "=&s"(x), [wa] "=&s"(wa), [wb] "=&s"(wb), [p] "=&s"(p)
         : [win] "v"(win)
         : "scc");
 #undef WX_RL_STEP
-    d = dd;
+    d += __popc(cm);
     return cm;
 }
 
@@ -1267,21 +1285,55 @@ __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
 // path moves at most 32 columns per block, so block b - 3 starts at most 64 columns left of
 // A and ends within 128 of it.  At use, the 64 lanes from the walk's offset are gathered
 // into one word per lane (two ds_bpermutes, skipped while the block fits the first word).
+// Speculative walk segments (multi-wave workgroups, T <= kMaxLdsFrames).  The blocks below the
+// top are cut into K segments of L blocks; the walker wave of segment k >= 1 starts at its top
+// block from a guessed column and records its column after every block (colrec), its result
+// and its end column.  Backtrack paths from different cells merge (Viterbi survivor paths),
+// and the walk is a function of (block, column) alone, so once the true walk (wave 0) stands
+// where segment k's walker stood after the same block — or enters segment k on its guessed
+// column — the rest of that segment's change masks, end column and result are the true
+// walk's, and wave 0 jumps to the segment's end.
+struct SpecWalk {
+    int K, L, L0, top;  // segments; blocks per segment (segment 0: L0)
+    const int* colrec;  // LDS, per block: the segment walker's column after it (-1: not reached)
+    const int* gstart;  // LDS [K]: guessed column at the top of segment k
+    const int* sres;    // LDS [K]: the walker's result (-2: the path continues below the segment)
+    const int* send;    // LDS [K]: its column after the segment's last block
+    __device__ __forceinline__ int lo(int k) const { return max(top - L0 - k * L + 1, 0); }
+};
+
+// The backtrack walk (alignment.py:395-421) over the decision bitmap: from column j at the
+// top of block b (steps above the start cleared by first_mask), step back one frame at a time
+// and move to the previous token where the decision bit is set.  Once j reaches 0 the window
+// reads cell 0 (all zero), so blocks run to completion without an early-exit test.  Per
+// block only the change mask is kept (cmask[b]); start frames are compacted from it
+// afterwards.  Returns the block where j reached 0, -1 where the reference returns None
+// (block 0 done with j > 0), or -2 when it stopped after block b_stop > 0 with the path
+// going on (column in j_out).  colrec (LDS, optional) receives the column after each block;
+// spec (optional) lets the walk jump over blocks a merged segment walker has done.
+//
+// The bitmap words are global loads (written by other waves or CUs), so the walk keeps three
+// blocks' windows in flight: the window of block b - 3 is issued when block b starts, at the
+// column A the walk has then; lane i loads the words of columns A - i and A - 64 - i.  The
+// path moves at most 32 columns per block, so block b - 3 starts at most 64 columns left of
+// A and ends within 128 of it.  At use, the 64 lanes from the walk's offset are gathered
+// into one word per lane (two ds_bpermutes, skipped while the block fits the first word).
 template <class LoadWin>  // LoadWin(b, A): this lane's word of column A - lane in block b (clamped)
-__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask, bool cmask_in_lds) {
-    if (t_start <= 0 || N <= 0) return -1;
+__device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsigned first_mask, int b_stop,
+                                          unsigned* cmask, bool cmask_in_lds, int* colrec, const SpecWalk* spec,
+                                          int& j_out, int wtop = 0x7fffffff, int* jentry = nullptr) {
     struct Win {
         unsigned lo, hi;
         int A;
     };
+    typedef __attribute__((address_space(3))) int lds_int;
     const int lane = lane_id();
-    int b = uniform((t_start - 1) >> 5);
-    int j = uniform(N);
-    unsigned first_mask = 0xFFFFFFFFu << (31 - ((t_start - 1) & 31));  // steps above t_start - 1
+    b = uniform(b);
+    j = uniform(j);
 #ifdef WX_PHASE_TIMING
     unsigned long long t_rl = 0, n_ch = 0, n_bl = 0;
     auto dump = [&]() {
-        if (lane == 0 && blockIdx.x < 8192) {
+        if (threadIdx.x == 0 && blockIdx.x < 8192) {  // (wave 0's last walk_range)
             unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + 13) * 3;
             o[0] = t_rl;
             o[1] = n_ch;
@@ -1293,13 +1345,25 @@ __device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start,
 #endif
     unsigned cmv = 0u;    // change masks of blocks gb + lane
     int gtop = b & 63;    // highest lane of the current group the walk has written
+    int sk = 0, slo = spec ? spec->lo(0) : 0;  // segment of the current block, its lowest block
+    auto flush = [&](int bb) {  // store the group's masks written since the last flush (blocks >= bb)
+        const int gb = bb & ~63;
+        if (lane >= (bb & 63) && lane <= gtop && gb + lane <= wtop) {
+            if (cmask_in_lds)
+                ((__attribute__((address_space(3))) unsigned*)cmask)[gb + lane] = cmv;
+            else
+                ((__attribute__((address_space(1))) unsigned*)cmask)[gb + lane] = cmv;
+        }
+        gtop = 63;
+    };
     auto issue = [&](Win& w, int bb, int A) {
         w.A = uniform(A);
         w.lo = load_win(bb, A);
         w.hi = load_win(bb, A - 64);
     };
-    // walks block b with window w; false when the walk is over (result in res)
-    auto block = [&](Win& w, int& res) -> bool {
+    // walks block b with window w (wn, wa: the next two blocks' windows, re-issued after a
+    // jump); false when the walk is over (result in res)
+    auto block = [&](Win& w, Win& wn, Win& wa, int& res) -> bool {
         const int d = uniform(w.A - j);  // 0 .. 96
         unsigned win;
         int dd;
@@ -1335,20 +1399,53 @@ __device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start,
         // pending load at each wait)
         cmv = lane == (b & 63) ? cm : cmv;
         j = uniform(j - (dd - d0));
-        const bool done = j <= 0 || b == 0;
-        if (done || (b & 63) == 0) {
-            const int gb = b & ~63;
-            if (lane >= (b & 63) && lane <= gtop) {
-                if (cmask_in_lds)
-                    ((__attribute__((address_space(3))) unsigned*)cmask)[gb + lane] = cmv;
-                else
-                    ((__attribute__((address_space(1))) unsigned*)cmask)[gb + lane] = cmv;
-            }
-            gtop = 63;
+        if (b > wtop) {  // (blocks above wtop: walked, not recorded)
+            if (b == wtop + 1) *jentry = j;
+        } else if (colrec && lane == 0) {
+            ((lds_int*)colrec)[b] = j;
         }
+        bool done = j <= 0 || b == 0 || b == b_stop;
+        int r = j <= 0 ? b : (b == 0 ? -1 : -2);
+        if (spec && !done) {
+            // merged with a segment walker: mid-segment on its recorded column, or at a segment's
+            // top on its guessed column; follow merged segments to the first one that is not
+            while (b < slo) slo = spec->lo(++sk);  // (b only moves down)
+            int k = sk;
+            int bb = b, jj = j;
+            bool merged = k >= 1 && bb != spec->lo(k) && jj == uniform(((const lds_int*)spec->colrec)[bb]);
+            for (;;) {
+                if (merged) {
+                    r = uniform(((const lds_int*)spec->sres)[k]);
+                    bb = spec->lo(k);
+                    jj = uniform(((const lds_int*)spec->send)[k]);
+                    if (r != -2) break;
+                }
+                merged = bb == spec->lo(k) && k + 1 < spec->K && jj == uniform(((const lds_int*)spec->gstart)[k + 1]);
+                if (!merged) break;
+                ++k;
+            }
+            if (bb != b) {  // jumped: the walk goes on after block bb (or is over: r)
+                flush(b);
+                if (r != -2) {
+                    res = r;
+                    dump();
+                    return false;
+                }
+                b = uniform(bb);
+                j = uniform(jj);
+                gtop = (b - 1) & 63;
+                issue(w, b - 3, j);
+                issue(wn, b - 1, j);
+                issue(wa, b - 2, j);
+                --b;
+                return true;
+            }
+        }
+        if (done || (b & 63) == 0) flush(b);
         issue(w, b - 3, j);  // unconditional (a conditional refill would merge and wait)
         if (done) {
-            res = j <= 0 ? b : -1;
+            res = r;
+            j_out = j;
             dump();
             return false;
         }
@@ -1356,21 +1453,89 @@ __device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start,
         return true;
     };
     Win w0, w1, w2;
-    issue(w0, b, N);
-    issue(w1, b - 1, N);
-    issue(w2, b - 2, N);
+    issue(w0, b, j);
+    issue(w1, b - 1, j);
+    issue(w2, b - 2, j);
     int res = -1;
     for (;;) {
-        if (!block(w0, res)) return res;
-        if (!block(w1, res)) return res;
-        if (!block(w2, res)) return res;
+        if (!block(w0, w1, w2, res)) return res;
+        if (!block(w1, w2, w0, res)) return res;
+        if (!block(w2, w0, w1, res)) return res;
     }
+}
+
+template <class LoadWin>
+__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask, bool cmask_in_lds) {
+    if (t_start <= 0 || N <= 0) return -1;
+    int jo;
+    return walk_range(load_win, N, (t_start - 1) >> 5, 0xFFFFFFFFu << (31 - ((t_start - 1) & 31)), 0, cmask,
+                      cmask_in_lds, nullptr, nullptr, jo);
 }
 
 template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
 __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
                     bool cmask_in_lds) {
     return walk_impl([&](int b, int A) { return load_window<CC>(bits, lay, b, A); }, N, t_start, cmask, cmask_in_lds);
+}
+
+// Speculative walk: blocks top..0 of a walk from (t_start, N) in K segments over the workgroup's
+// first K waves (SpecWalk).  Phase 1: wave 0 walks the top segment; wave k starts kSpecOverlap
+// blocks above its segment from a guessed column and walks those blocks unrecorded, so that
+// its path has usually merged with the true one when it enters the segment (its entry column
+// is gstart[k]).  Phase 2 (after a workgroup barrier): wave 0 goes on from the top segment's
+// end, jumping over whatever merged — usually every segment, with no block walked again.
+// Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
+// block, or -1), meaningful in wave 0.
+constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
+constexpr int kSpecOverlap = 2;    // unrecorded blocks a segment walker starts above its segment
+template <int CC>
+__device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
+                         int K, int* colrec, int* sbuf) {
+    auto lw = [&](int b, int A) { return load_window<CC>(bits, lay, b, A); };
+    const int wv = uniform((int)threadIdx.x >> 6);
+    const int lane = lane_id();
+    SpecWalk sw;
+    sw.top = (t_start - 1) >> 5;
+    sw.K = K;
+    sw.L = max((sw.top + 1 - kSpecOverlap + K - 1) / K, 1);
+    sw.L0 = sw.L + kSpecOverlap;  // (balances wave 0's segment with the walkers' overlap + segment)
+    sw.colrec = colrec;
+    sw.gstart = sbuf;
+    sw.sres = sbuf + K;
+    sw.send = sbuf + 2 * K;
+    int res = -1, jo = 0;
+    if (wv == 0) {
+        res = walk_range(lw, N, sw.top, 0xFFFFFFFFu << (31 - ((t_start - 1) & 31)), sw.lo(0), cmask, true, nullptr,
+                         nullptr, jo);
+    } else if (wv < K) {
+        const int top = sw.lo(wv - 1) - 1, lo = sw.lo(wv), sb = top + kSpecOverlap;
+        // guess: the straight line from (0, 0) to (t_start, N), inside the cells the path can
+        // occupy at time 32 (sb + 1) (column <= time, N - column <= remaining steps)
+        const int tt = 32 * (sb + 1);
+        int g = (int)(((int64_t)N * tt + t_start / 2) / t_start);
+        g = min(max(g, max(1, N - (t_start - tt))), min(N, tt));
+        for (int bb = lo + lane; bb <= top; bb += kWave) colrec[bb] = -1;
+        int je = -1;  // column entering the segment (-1: the path ended above it)
+        const int r = walk_range(lw, g, sb, 0xFFFFFFFFu, lo, cmask, true, colrec, nullptr, jo, top, &je);
+        if (lane == 0) {
+            sbuf[wv] = je;
+            sbuf[K + wv] = r;
+            sbuf[2 * K + wv] = jo;
+        }
+    }
+    wave_fence();
+    block_fence();
+    if (wv == 0 && res == -2) {
+        // segments entered on their guessed column are the true walk's as a whole
+        int k = 1;
+        for (; k < K && jo == uniform(sbuf[k]); ++k) {
+            res = uniform(sbuf[K + k]);
+            jo = uniform(sbuf[2 * K + k]);
+            if (res != -2) return res;
+        }
+        res = walk_range(lw, jo, sw.lo(k - 1) - 1, 0xFFFFFFFFu, 0, cmask, true, nullptr, &sw, jo);
+    }
+    return res;
 }
 
 // start[k] = k-th change frame in increasing time: a popcount prefix over the change masks
@@ -1425,17 +1590,6 @@ __device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* 
 
 // Order one wave's own global/LDS writes before its later reads by other lanes (no
 // barrier: safe inside wave-divergent regions of multi-wave workgroups).
-__device__ __forceinline__ void wave_fence() {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ __forceinline__ void block_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 // (cells per lane C, DP waves per segment W, helper wave H) buckets, one kernel
 // instantiation each; id = C << 8 | W << 1 | H.
@@ -1594,6 +1748,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
     __shared__ int argred[3 * (W + H)];
+    __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
+    __shared__ int sbuf_lds[3 * (W + H)];
     __shared__ ColMapLds<VS> cml;
     const int P = SP ? a.parts : 1;
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
@@ -1691,17 +1847,21 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 #endif
     // t_start: with every wave when the workgroup has several (the walk waits for it)
     const int ts_block = (W + H > 1) ? block_argmax(cn, d.T, argred) : 0;
+#ifdef WX_PHASE_TIMING
+    WX_T(w1);
+#endif
+    // several waves: the walk's blocks in speculative segments, one per wave (walk_spec)
+    const int nbw = ts_block > 0 ? ((ts_block - 1) >> 5) + 1 : 0;
+    const int K = (W + H > 1 && d.T <= kMaxLdsFrames && d.N > 0) ? min(W + H, nbw / kSpecMinBlocks) : 1;
+    const int b_lo_spec = K >= 2 ? walk_spec<C>(bits, lay, d.N, ts_block, cmask_lds, K, colrec_lds, sbuf_lds) : -1;
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
         const int ts = (W + H > 1) ? ts_block : column_argmax(cn, d.T);
-#ifdef WX_PHASE_TIMING
-        WX_T(w1);
-#endif
         if (lane == 0) {
             a.t_start[seg] = ts;
             tsb[0] = ts;
         }
         unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = walk<C>(bits, lay, d.N, ts, cmask, d.T <= kMaxLdsFrames);
+        const int b_lo = K >= 2 ? b_lo_spec : walk<C>(bits, lay, d.N, ts, cmask, d.T <= kMaxLdsFrames);
 #ifdef WX_PHASE_TIMING
         WX_T(w2);
 #endif
