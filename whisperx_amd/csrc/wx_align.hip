@@ -1487,7 +1487,10 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
 // Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
 // block, or -1), meaningful in wave 0.
 constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
-constexpr int kSpecOverlap = 2;    // unrecorded blocks a segment walker starts above its segment
+#ifndef WX_SPEC_OVERLAP
+#define WX_SPEC_OVERLAP 2
+#endif
+constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker starts above its segment
 template <int CC>
 __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
                          int K, int* colrec, int* sbuf) {
