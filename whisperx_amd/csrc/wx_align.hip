@@ -1491,32 +1491,55 @@ constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
 #define WX_SPEC_OVERLAP 2
 #endif
 constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker starts above its segment
+#ifndef WX_SPEC_EARLY
+#define WX_SPEC_EARLY 1
+#endif
+constexpr int kSpecArgmaxBlocks = 3;  // wave 0's t_start search, in walk blocks (WX_SPEC_EARLY)
 template <int CC>
-__device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
-                         int K, int* colrec, int* sbuf) {
+__device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int T, const float* cn,
+                         int* argred, unsigned* cmask, int K, int* colrec, int* sbuf, int& t_start) {
     auto lw = [&](int b, int A) { return load_window<CC>(bits, lay, b, A); };
     const int wv = uniform((int)threadIdx.x >> 6);
     const int lane = lane_id();
     SpecWalk sw;
-    sw.top = (t_start - 1) >> 5;
     sw.K = K;
-    sw.L = max((sw.top + 1 - kSpecOverlap + K - 1) / K, 1);
-    sw.L0 = sw.L + kSpecOverlap;  // (balances wave 0's segment with the walkers' overlap + segment)
     sw.colrec = colrec;
     sw.gstart = sbuf;
     sw.sres = sbuf + K;
     sw.send = sbuf + 2 * K;
-    int res = -1, jo = 0;
+    int res = -1, jo = 0, tb = 0;
+    unsigned fm = 0u;
+#if WX_SPEC_EARLY
+    // The segments cover the blocks below T (t_start <= T): the walkers start while wave 0
+    // alone finds t_start, so its segment is kSpecArgmaxBlocks shorter than theirs.
+    sw.top = (T - 1) >> 5;
+    sw.L = max((sw.top + 1 + kSpecArgmaxBlocks + K - 1) / K, 1);
+    sw.L0 = max(sw.L - kSpecArgmaxBlocks, 1);
+    const int tref = T;
+    if (wv == 0) t_start = column_argmax(cn, T);
+#else
+    t_start = block_argmax(cn, T, argred);
+    sw.top = (t_start - 1) >> 5;
+    sw.L = max((sw.top + 1 - kSpecOverlap + K - 1) / K, 1);
+    sw.L0 = sw.L + kSpecOverlap;  // (balances wave 0's segment with the walkers' overlap + segment)
+    const int tref = t_start;
+#endif
     if (wv == 0) {
-        res = walk_range(lw, N, sw.top, 0xFFFFFFFFu << (31 - ((t_start - 1) & 31)), sw.lo(0), cmask, true, nullptr,
-                         nullptr, jo);
+        if (t_start <= 0) {
+            res = -1;  // (the reference's None)
+        } else {
+            tb = (t_start - 1) >> 5;
+            fm = 0xFFFFFFFFu << (31 - ((t_start - 1) & 31));
+            res = tb >= sw.lo(0) ? walk_range(lw, N, tb, fm, sw.lo(0), cmask, true, nullptr, nullptr, jo)
+                                 : -3;  // starts in a lower segment: after the barrier
+        }
     } else if (wv < K) {
         const int top = sw.lo(wv - 1) - 1, lo = sw.lo(wv), sb = top + kSpecOverlap;
-        // guess: the straight line from (0, 0) to (t_start, N), inside the cells the path can
+        // guess: the straight line from (0, 0) to (tref, N), inside the cells the path can
         // occupy at time 32 (sb + 1) (column <= time, N - column <= remaining steps)
         const int tt = 32 * (sb + 1);
-        int g = (int)(((int64_t)N * tt + t_start / 2) / t_start);
-        g = min(max(g, max(1, N - (t_start - tt))), min(N, tt));
+        int g = (int)(((int64_t)N * tt + tref / 2) / tref);
+        g = min(max(g, max(1, N - (tref - tt))), min(N, tt));
         for (int bb = lo + lane; bb <= top; bb += kWave) colrec[bb] = -1;
         int je = -1;  // column entering the segment (-1: the path ended above it)
         const int r = walk_range(lw, g, sb, 0xFFFFFFFFu, lo, cmask, true, colrec, nullptr, jo, top, &je);
@@ -1537,6 +1560,8 @@ __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, i
             if (res != -2) return res;
         }
         res = walk_range(lw, jo, sw.lo(k - 1) - 1, 0xFFFFFFFFu, 0, cmask, true, nullptr, &sw, jo);
+    } else if (wv == 0 && res == -3) {
+        res = walk_range(lw, N, tb, fm, 0, cmask, true, nullptr, &sw, jo);
     }
     return res;
 }
@@ -1849,16 +1874,19 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     WX_T(w0);
 #endif
     // t_start: with every wave when the workgroup has several (the walk waits for it)
-    const int ts_block = (W + H > 1) ? block_argmax(cn, d.T, argred) : 0;
+    // several waves: the walk's blocks in speculative segments, one per wave (walk_spec, which
+    // also finds t_start)
+    const int nbw = ((d.T - 1) >> 5) + 1;
+    const int K = (W + H > 1 && d.T <= kMaxLdsFrames && d.N > 0) ? min(W + H, nbw / kSpecMinBlocks) : 1;
+    const int ts_block = (W + H > 1 && K < 2) ? block_argmax(cn, d.T, argred) : 0;
 #ifdef WX_PHASE_TIMING
     WX_T(w1);
 #endif
-    // several waves: the walk's blocks in speculative segments, one per wave (walk_spec)
-    const int nbw = ts_block > 0 ? ((ts_block - 1) >> 5) + 1 : 0;
-    const int K = (W + H > 1 && d.T <= kMaxLdsFrames && d.N > 0) ? min(W + H, nbw / kSpecMinBlocks) : 1;
-    const int b_lo_spec = K >= 2 ? walk_spec<C>(bits, lay, d.N, ts_block, cmask_lds, K, colrec_lds, sbuf_lds) : -1;
+    int ts_spec = 0;
+    const int b_lo_spec =
+        K >= 2 ? walk_spec<C>(bits, lay, d.N, d.T, cn, argred, cmask_lds, K, colrec_lds, sbuf_lds, ts_spec) : -1;
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
-        const int ts = (W + H > 1) ? ts_block : column_argmax(cn, d.T);
+        const int ts = K >= 2 ? ts_spec : (W + H > 1) ? ts_block : column_argmax(cn, d.T);
         if (lane == 0) {
             a.t_start[seg] = ts;
             tsb[0] = ts;
