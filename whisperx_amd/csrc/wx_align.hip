@@ -1494,7 +1494,10 @@ constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker sta
 #ifndef WX_SPEC_EARLY
 #define WX_SPEC_EARLY 1
 #endif
-constexpr int kSpecArgmaxBlocks = 3;  // wave 0's t_start search, in walk blocks (WX_SPEC_EARLY)
+#ifndef WX_SPEC_ARGMAX_BLOCKS
+#define WX_SPEC_ARGMAX_BLOCKS 3
+#endif
+constexpr int kSpecArgmaxBlocks = WX_SPEC_ARGMAX_BLOCKS;  // wave 0's t_start search, in walk blocks
 template <int CC>
 __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int T, const float* cn,
                          int* argred, unsigned* cmask, int K, int* colrec, int* sbuf, int& t_start) {
