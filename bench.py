@@ -152,8 +152,8 @@ def mae_vs_oracle(ems_np, toks, plan):
     for i, (em, tk) in enumerate(zip(ems_np, toks)):
         ok, tso, sso, seo, sco = oracle.align_dp(em, tk, 0)
         a, b = plan.b.tok_off[i], plan.b.tok_off[i + 1]
-        if not ok or st[i] != 0:
-            n_bad_path += int(ok != (st[i] == 0))
+        if not ok or (st[i] & 15) != 0:
+            n_bad_path += int(ok != ((st[i] & 15) == 0))
             continue
         ratio_ms = 1000.0 * FRAME_S
         errs.append(np.abs(ss[a:b] - sso) * ratio_ms)

@@ -59,6 +59,11 @@ enum {
                                       the blank and its token ids) */
 #define WX_MAX_TOKENS 16000  /* tokens per segment (8 waves x 64 lanes x 32 cells, less halos) */
 
+/* wx_align_dp status word: low bits = outcome, high bits = how the segment was computed */
+#define WX_STATUS_MASK 15        /* 0 aligned, 1 None, 2 / 3 not computed (see wx_align_dp) */
+#define WX_STATUS_RECOVERED 16   /* recomputed by the generic forward after a lost hand-off */
+#define WX_STATUS_GENERIC 32     /* computed by the generic forward (> 256 distinct columns) */
+
 const char* wx_version(void);
 const char* wx_strerror(int code);
 
@@ -95,13 +100,18 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
  * (never materialised), argmax, backtrack and merge_repeats.  Outputs are CSR by tok_off:
  * seg_start/seg_end (frames, end exclusive) and seg_score of token k (the k-th
  * merge_repeats segment; a successful path always yields exactly N_s of them).
- * t_start[s] as above; status[s] = 0 aligned, 1 backtrack failed (reference: None).
+ * t_start[s] as above; status[s] & WX_STATUS_MASK = 0 aligned, 1 backtrack failed
+ * (reference: None).
  * Segments the fast kernels cannot finish are recomputed in-kernel by a generic (slow,
- * barrier-per-step) forward with the same arithmetic: a split segment whose cross-CU
- * hand-off timed out, and a V > 64 segment using more than WX_MAX_SEGMENT_COLUMNS distinct
- * emission columns.  Only when that forward's LDS rows cannot hold the segment either
- * (3 (N + 1) floats > ~84 KB, i.e. N > ~7000 such tokens) is the segment reported
- * 2 (too many columns) or 3 (hand-off lost) and left uncomputed.
+ * barrier-per-step, ~1-3 ms per 30 s segment) forward with the same arithmetic, and say so
+ * in status's flag bits: WX_STATUS_RECOVERED for a split segment whose cross-CU hand-off
+ * timed out (transient starvation: another launch held the CUs), WX_STATUS_GENERIC for a
+ * V > 64 segment using more than WX_MAX_SEGMENT_COLUMNS distinct emission columns.  That
+ * forward keeps two rows and one decision word per cell in the kernel's LDS (3 (N + 1)
+ * floats), so it holds N <= 5460 tokens in the one-wave (throughput) buckets of V > 64,
+ * N <= 7167 in the latency / split buckets of V <= 64 and N <= 10921 in those of V > 64.
+ * Beyond that the segment is left uncomputed and reported 2 (too many columns: split the
+ * segment) or 3 (hand-off lost: re-running the call normally succeeds).
  * min_N/max_N/sum_T describe the batch (host values).
  * Split launches hand halo cells between CUs through a hand-off region of granules tagged
  * with the launch's 32-bit epoch, plus per-segment arrival counters.  wx_align_dp /

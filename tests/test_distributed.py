@@ -81,3 +81,31 @@ def test_gloo_world2_broadcast_and_gather():
     for r in (0, 1):
         for i in shards[r]:
             assert merged[i] == {"file": f"f{i}", "rank": r}
+
+
+@pytest.mark.gpu
+def test_rccl_world1_device_broadcast_and_allreduce():
+    """The RCCL branch on the GPU: a world-size-1 "nccl" (= RCCL) group, the dictionary's
+    device-tensor broadcast (forced past the world-of-one shortcut) and bench._allreduce on
+    device tensors (max and sum) — the collectives the 8-GPU bench runs, on one GPU."""
+    import bench
+
+    assert torch.cuda.is_available()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        vocab = {"<pad>": 0, "|": 4, "e": 5, "ß": 37, "日": 41}
+        assert broadcast_dictionary(vocab, device=dev, force=True) == vocab
+        old = bench._allreduce.dev
+        bench._allreduce.dev = dev
+        try:
+            assert bench._allreduce([1.5, -2.0], "max") == [1.5, -2.0]
+            assert bench._allreduce([3.0, 4.0], "sum") == [3.0, 4.0]
+        finally:
+            bench._allreduce.dev = old
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

@@ -37,21 +37,85 @@ def test_channel_norm_vs_torch_groupnorm(L, C, gelu):
     assert torch.equal(inplace, got)
 
 
-def test_prepared_wav2vec2_forward_matches_stock():
-    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
-
+def _check_prepared_vs_stock(m, V, lengths, tol=5e-5):
     from whisperx_amd import emission
 
-    torch.manual_seed(0)
-    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
     rng = np.random.default_rng(0)
-    for n in (400, 7 * 16000 + 123, 30 * 16000):
+    worst = 0.0
+    for n in lengths:
         x = torch.from_numpy(rng.standard_normal(n).astype(np.float32) * 0.1)[None].cuda()
         with torch.inference_mode():
             ref = torch.log_softmax(m(x).logits, -1)
             emission.prepare_model(m)
             got = torch.log_softmax(m(x).logits, -1)
             emission.restore_model(m)
-        assert got.shape == ref.shape == (1, emission.n_frames(n), 32)
-        assert float((got - ref).abs().max()) < 5e-5
-        assert torch.equal(got.argmax(-1), ref.argmax(-1))
+        assert got.shape == ref.shape == (1, emission.n_frames(n, m), V)
+        err = float((got - ref).abs().max())
+        worst = max(worst, err)
+        assert err < tol, f"{n} samples: max |prepared - stock| = {err}"
+        assert torch.equal(got.argmax(-1), ref.argmax(-1)), f"{n} samples: frame argmax differs"
+    return worst
+
+
+def test_prepared_wav2vec2_forward_matches_stock():
+    """Group-norm feature encoder (wav2vec2-base-960h, the torchaudio/HF English defaults)."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    torch.manual_seed(0)
+    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
+    _check_prepared_vs_stock(m, 32, (400, 7 * 16000 + 123, 30 * 16000))
+
+
+def large_xlsr_config(V=40):
+    """The layer-norm wav2vec2 family of the HF default alignment models (alignment.py:32-61:
+    every DEFAULT_ALIGN_MODELS_HF entry but `vi` is a large-xlsr / xls-r checkpoint, and
+    BASELINE config 5 names DE wav2vec2-large-xlsr): feat_extract_norm="layer" (a LayerNorm
+    after every feature-encoder conv), stable layer norm, conv bias."""
+    from transformers import Wav2Vec2Config
+
+    return Wav2Vec2Config(vocab_size=V, hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                          intermediate_size=4096, feat_extract_norm="layer", do_stable_layer_norm=True,
+                          conv_bias=True)
+
+
+def test_prepared_large_xlsr_forward_matches_stock():
+    """The GEMM-route convolutions on the layer-norm family (no GroupNorm layer: every conv
+    of the feature encoder takes the plain GEMM route, LayerNorm runs on its time-major
+    output): 400 samples, 7.3 s and 60 s (config 5's T = 2999)."""
+    from transformers import Wav2Vec2ForCTC
+
+    torch.manual_seed(1)
+    m = Wav2Vec2ForCTC(large_xlsr_config()).cuda().eval()
+    assert m.config.feat_extract_norm == "layer"
+    worst = _check_prepared_vs_stock(m, 40, (400, int(7.3 * 16000), 60 * 16000))
+    print(f"large-xlsr prepared vs stock: max |dlogp| = {worst:.3g}")
+
+
+def test_emissions_fan_out_fresh_parametrised_model():
+    """the positional conv's weight_norm weight is cached; on a freshly
+    built model the cache must exist before the forwards fan out over 8 streams, or the
+    streams read it before it is computed.  Segment 0 is much longer than the others (its
+    stream would still be building the weight when the others reach the positional conv).
+    Every segment's emission must equal a single-stream forward of the same model."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    from whisperx_amd import alignment, emission
+
+    torch.manual_seed(2)
+    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
+    pos = m.wav2vec2.encoder.pos_conv_embed.conv
+    assert getattr(pos, "parametrizations", None) is not None and not hasattr(pos, "_wx_w_cache")
+    g = torch.Generator().manual_seed(3)
+    audio = (torch.randn(1, 80 * 16000, generator=g) * 0.1).cuda()
+    wavs = [audio[:, : 60 * 16000]] + [audio[:, 16000 * k: 16000 * k + 16000 + 1234 * k] for k in range(1, 12)]
+    csr = alignment._emissions(m, "huggingface", wavs, "cuda:0", n_streams=8)
+    main = torch.cuda.current_stream()
+    for st in csr.streams:
+        main.wait_stream(st)
+    torch.cuda.synchronize()
+    with torch.inference_mode():
+        for i, w in enumerate(wavs):
+            ref = torch.log_softmax(m(w).logits, -1)[0]
+            err = float((csr[i] - ref).abs().max())
+            assert err <= 1e-6, f"segment {i}: fan-out emission differs from single-stream by {err}"
+    emission.restore_model(m)

@@ -59,7 +59,7 @@ def test_align_dp_matches_reference_golden(dp_cases):
         for s, (i, c) in enumerate(items):
             assert ts[s] == int(c["t_start"]), f"case {i}: t_start {ts[s]} != {int(c['t_start'])}"
             ok = int(c["path_ok"]) == 1
-            assert (st[s] == 0) == ok, f"case {i}: status {st[s]}"
+            assert st[s] == (0 if ok else 1), f"case {i}: status {st[s]}"
             if not ok:
                 continue
             a, e = b.tok_off[s], b.tok_off[s + 1]
@@ -91,16 +91,18 @@ def _random_cases(rng, n, T_range, N_range, V, quant=None, blank=None):
     return cases
 
 
-def _check_vs_oracle(cases, tag, mode=-1):
+def _check_vs_oracle(cases, tag, mode=-1, status_out=None):
     from whisperx_amd import _lib
 
     b = _batch(cases)
     ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b, mode=mode))
+    if status_out is not None:
+        status_out.append(st[: b.S].copy())
     mism = 0
     for s, c in enumerate(cases):
         ok, tso, sso, seo, sco = oracle.align_dp(c["em"], c["tokens"], int(c["blank"]))
         assert ts[s] == tso, f"{tag} seg {s}: t_start {ts[s]} vs {tso}"
-        assert (st[s] == 0) == ok, f"{tag} seg {s}: status"
+        assert bool(_lib.status_ok(st[s])) == ok, f"{tag} seg {s}: status {st[s]}"
         if ok:
             a, e = b.tok_off[s], b.tok_off[s + 1]
             assert np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo), f"{tag} seg {s}: spans"
@@ -246,22 +248,38 @@ def test_align_dp_large_vocabulary_too_many_columns(mode):
     tie = _large_vocab_cases(rng, 1000, 1, (300, 400), (280, 290), 300)
     tie[0]["em"] = (np.round(tie[0]["em"] * 16) / 16).astype(np.float32)  # exact ties
     nofit = _large_vocab_cases(rng, 1000, 1, (10, 40), (300, 320), 300)  # N > T: backtrack fails
-    _check_vs_oracle([ok_cases[0], big[0], ok_cases[1], big[1], tie[0], nofit[0]], f"many columns mode {mode}", mode)
+    sts = []
+    cases = [ok_cases[0], big[0], ok_cases[1], big[1], tie[0], nofit[0]]
+    _check_vs_oracle(cases, f"many columns mode {mode}", mode, status_out=sts)
+    from whisperx_amd import _lib
+
+    wide = [len(set(c["tokens"].tolist()) | {0, int(c["blank"])}) > _lib.MAX_SEGMENT_COLUMNS for c in cases]
+    assert wide[1] and wide[3] and not wide[0]
+    generic = (sts[0] & _lib.STATUS_GENERIC) != 0  # the route is reported per segment
+    assert generic.tolist() == wide, sts[0]
 
 
 def test_align_dp_lost_handoff_recovered(monkeypatch):
     """A split segment whose cross-CU hand-off is lost (WX_SPIN_LIMIT=0: no consumer part
     waits for its predecessor) is recomputed in-kernel by the last part to arrive; results
-    still equal the oracle, in the auto (split) shape and every explicit split."""
+    still equal the oracle, in the auto (split) shape and every explicit split, and every
+    such segment carries WX_STATUS_RECOVERED (none does once the hand-offs wait again)."""
+    from whisperx_amd import _lib
+
     rng = np.random.default_rng(12)
     cases = _random_cases(rng, 12, (1400, 1600), (300, 500), 32)
     cases += _random_cases(rng, 2, (2900, 3000), (850, 950), 32)
     cases += _random_cases(rng, 2, (20, 200), (10, 60), 32, quant=16)
     monkeypatch.setenv("WX_SPIN_LIMIT", "0")
     for mode in (-1, 12, 13, 14):
-        _check_vs_oracle(cases, f"lost hand-offs mode {mode}", mode)
+        sts = []
+        _check_vs_oracle(cases, f"lost hand-offs mode {mode}", mode, status_out=sts)
+        rec = (sts[0] & _lib.STATUS_RECOVERED) != 0
+        assert rec[:12].all(), f"mode {mode}: 30 s split segments not flagged recovered: {sts[0]}"
     monkeypatch.delenv("WX_SPIN_LIMIT")
-    _check_vs_oracle(cases, "after recovery", -1)
+    sts = []
+    _check_vs_oracle(cases, "after recovery", -1, status_out=sts)
+    assert int(((sts[0] & _lib.STATUS_RECOVERED) != 0).sum()) == 0, sts[0]
 
 
 def test_align_dp_handoff_region_reuse():
@@ -281,8 +299,8 @@ def test_align_dp_handoff_region_reuse():
     for _ in range(3):
         plan.run()
     torch.cuda.synchronize()
-    xg = plan.hob - (b.S + 1) * 4
-    arrive = plan.ho[plan.hob - ((b.S + 1) * 4 + 255) // 256 * 256:].view(torch.int32)[: b.S]
+    xg = plan.hob - (b.S + 1) * 8
+    arrive = plan.ho[plan.hob - ((b.S + 1) * 8 + 255) // 256 * 256:].view(torch.int64)[: b.S]
     assert int(arrive.count_nonzero()) == 0 and xg > 0
     # a workspace full of tag-like garbage through the memset path
     lib = _lib.load()
@@ -497,6 +515,22 @@ def test_align_end_to_end_matches_reference(si, capsys):
     assert jsonable(mutated) == sc["mutated"]
     if stats.get("abs_err"):
         assert float(np.mean(stats["abs_err"])) * 1000 <= 1.0  # word-boundary MAE (ms)
+
+
+@pytest.mark.parametrize("si", range(len(scenarios())))
+def test_align_device_cpu_matches_reference(si, capsys):
+    """Config 1's literal call, align(..., device='cpu'): the model forward and log_softmax on
+    the CPU (alignment.py:226-235 with device='cpu'), the DP on GPU 0 (_dp_device), the
+    emissions copied over once per group.  Same golden results as the reference."""
+    from whisperx_amd import align
+
+    sc, logits = scenarios()[si]
+    stats = {}
+    out, mutated = run_scenario(align, sc, logits, "cpu")
+    compare(jsonable(out), sc["result"], time_tol=0.02 + 1e-9, score_tol=1e-3 + 1e-9, stats=stats)
+    assert jsonable(mutated) == sc["mutated"]
+    if stats.get("abs_err"):
+        assert float(np.mean(stats["abs_err"])) * 1000 <= 1.0
 
 
 # ------------------------------------------------------------------------------ VAD

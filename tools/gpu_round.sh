@@ -6,7 +6,9 @@ set -o pipefail
 TAG=${1:-x}; shift
 O=gpurun_out
 mkdir -p $O
-for step in "${@:-tests bench}"; do
+steps=("$@")
+[ ${#steps[@]} -eq 0 ] && steps=(tests bench)
+for step in "${steps[@]}"; do
   case $step in
     tests) timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/${TAG}_gputests.log 2>&1 || { echo "tests failed"; tail -30 $O/${TAG}_gputests.log; exit 1; } ; tail -3 $O/${TAG}_gputests.log ;;
     bench) timeout -k 10 600 python bench.py > $O/${TAG}_bench.log 2>&1 || { echo "bench failed"; tail -30 $O/${TAG}_bench.log; exit 1; } ; tail -1 $O/${TAG}_bench.log | cut -c1-600 ;;

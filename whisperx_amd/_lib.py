@@ -24,6 +24,25 @@ INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 MAX_VOCAB = 16384
 MAX_SEGMENT_COLUMNS = 256  # V > 64: distinct emission columns one segment may use
 MAX_TOKENS = 16000
+# wx_align_dp status word (include/wx_align.h): outcome in the low bits, route flags above
+STATUS_MASK, STATUS_RECOVERED, STATUS_GENERIC = 15, 16, 32
+
+
+def status_ok(status):
+    """Aligned segments of a status array (numpy or torch): outcome 0, whatever the flags."""
+    return (status & STATUS_MASK) == 0
+
+
+def status_summary(status) -> dict:
+    """Counts of a status array: aligned, None, and the segments the in-kernel generic
+    forward computed (recovered after a lost hand-off / too many columns)."""
+    import numpy as np
+    st = status.cpu().numpy() if torch.is_tensor(status) else np.asarray(status)
+    out = st & STATUS_MASK
+    return {"aligned": int((out == 0).sum()), "none": int((out == 1).sum()),
+            "not_computed": int((out >= 2).sum()),
+            "recovered_segments": int(((st & STATUS_RECOVERED) != 0).sum()),
+            "generic_forward_segments": int(((st & STATUS_GENERIC) != 0).sum())}
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

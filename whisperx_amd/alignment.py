@@ -293,6 +293,9 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
         return [_emission(model, model_type, w, device) for w in waveforms]
     if not os.environ.get("WX_MIOPEN_CONV"):
         emission.prepare_model(model)
+        # cached weight_norm weights are built here, on the current stream, before the
+        # side streams wait on it (a lazily built cache would race between the streams)
+        emission.materialize_weights(model)
     V = _vocab_size(model, model_type)
     cfg_model = model if model_type == "huggingface" else None
     Ts = [emission.n_frames(int(w.shape[-1]), cfg_model) for w in waveforms]
@@ -494,15 +497,25 @@ def _run_dp(ems, toks, blanks, dev):
     se = seg_end.cpu().numpy()
     sc = seg_score.cpu().numpy()
     st = status.cpu().numpy()
-    if (st >= 2).any():  # the in-kernel generic forward could not hold the segment either
-        i = int(np.flatnonzero(st >= 2)[0])
-        raise _lib.WXError(f"segment {i} ({batch.Ns[i]} tokens) is too long for the recovery forward "
-                           f"(status {int(st[i])}); split it into shorter segments")
+    outcome = st & _lib.STATUS_MASK
+    if (outcome >= 2).any():  # the in-kernel generic forward could not hold the segment either
+        i = int(np.flatnonzero(outcome >= 2)[0])
+        if outcome[i] == 3:
+            raise _lib.WXError(f"segment {i} ({batch.Ns[i]} tokens): a cross-CU hand-off was lost and the segment "
+                               f"is too long for the in-kernel recovery forward (status 3); this is transient "
+                               f"(the GPU was busy with other work), re-running the call normally succeeds")
+        raise _lib.WXError(f"segment {i} ({batch.Ns[i]} tokens) uses more than {_lib.MAX_SEGMENT_COLUMNS} distinct "
+                           f"emission columns and is too long for the generic forward (status 2); split it into "
+                           f"shorter segments")
+    _run_dp.recovered += int(((st & _lib.STATUS_RECOVERED) != 0).sum())
     out = []
     for i in range(batch.S):
         a, b = batch.tok_off[i], batch.tok_off[i + 1]
-        out.append((st[i] == 0, ss[a:b], se[a:b], sc[a:b], batch.Ts[i]))
+        out.append((outcome[i] == 0, ss[a:b], se[a:b], sc[a:b], batch.Ts[i]))
     return out
+
+
+_run_dp.recovered = 0  # segments recomputed after a lost hand-off, over the process (bench legs report it)
 
 
 # ------------------------------------------------------------------ host post-processing

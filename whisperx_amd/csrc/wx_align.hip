@@ -1720,20 +1720,25 @@ struct AlignArgs {
     int split_id;    // split launches: the one split bucket (segments up to its capacity)
     unsigned epoch;  // split launches: per-launch tag of the hand-off granules and counters
     uint64_t* xg;    // workspace: hand-off granules, (floor(row0/32) + seg + q) * 3 * 40
-    unsigned* arrive;// workspace: per-segment arrival counters (epoch << 8 | count)
+    uint64_t* arrive;// workspace: per-segment arrival counters {count, epoch} (split_arrive)
     int spin;        // split launches: hand-off re-reads before a part counts as lost
 };
 
-// Per-segment arrival of a split segment's parts; true for the last to arrive.  The word
-// is epoch << 8 | count (bit 7: a part lost a hand-off), so stale or uninitialised
-// workspace never needs clearing.  Returns the word after this arrival.
-__device__ unsigned split_arrive(unsigned* c, unsigned epoch, bool lost) {
-    const unsigned ep = epoch & 0xFFFFFFu;
-    unsigned old = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Per-segment arrival of a split segment's parts.  The counter is one 8-byte word,
+// {low: count | 0x80 if a part lost a hand-off, high: the launch's full 32-bit epoch}, so a
+// word left by anything else never matches: a zeroed word has epoch 0 (never issued), an
+// older launch's counter has an older epoch, and — the hand-off region being reused across
+// batch layouts — an 8-byte hand-off granule that now sits where a counter lands carries
+// its own launch's epoch in the same high half.  (Round 2 matched 24 epoch bits of a 4-byte
+// word, which a granule's float half could match by chance.)  Returns the low word after
+// this arrival.
+__device__ unsigned split_arrive(uint64_t* c, unsigned epoch, bool lost) {
+    uint64_t old = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (true) {
-        const unsigned cur = ((old >> 8) == ep) ? (old & 0xFFu) : 0u;
-        const unsigned nw = (ep << 8) | ((cur & 0x7Fu) + 1u) | (cur & 0x80u) | (lost ? 0x80u : 0u);
-        if (__hip_atomic_compare_exchange_strong(c, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+        const unsigned cur = ((unsigned)(old >> 32) == epoch) ? (unsigned)old : 0u;
+        const unsigned nw = ((cur & 0x7Fu) + 1u) | (cur & 0x80u) | (lost ? 0x80u : 0u);
+        const uint64_t nv = ((uint64_t)epoch << 32) | nw;
+        if (__hip_atomic_compare_exchange_strong(c, &old, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT))
             return nw;
     }
@@ -1845,7 +1850,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 wait_vm();
                 // every part has arrived: leave the counter clean for the next launch
-                __hip_atomic_store(a.arrive + seg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.arrive + seg, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
@@ -1921,7 +1926,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     const int ts = tsb[0];
     const bool ok = tsb[1] != 0;
     WX_STAMP(2);
-    if (lane == 0) a.status[seg] = ok ? 0 : 1;
+    // low bits: 0 aligned / 1 None; flags: which segments took the generic forward
+    if (lane == 0) a.status[seg] = (ok ? 0 : 1) | (failed ? WX_STATUS_RECOVERED : 0) | (slow ? WX_STATUS_GENERIC : 0);
     if (!ok) return;
     merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
     WX_STAMP(3);
@@ -2607,7 +2613,7 @@ size_t cn_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T + 4 *
 size_t xg_bytes(int32_t S, int64_t sum_T) {
     return align_up((size_t)(sum_T / kChunk + S + 2) * (kMaxParts - 1) * kHaloCells * 8u, 256);
 }
-size_t arrive_bytes(int32_t S) { return align_up((size_t)(S + 1) * 4u, 256); }
+size_t arrive_bytes(int32_t S) { return align_up((size_t)(S + 1) * 8u, 256); }
 
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
     return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T) +
@@ -2712,7 +2718,7 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
                                           align_up((size_t)(sum_T + 1) * 4u, 256));
     a.cn = reinterpret_cast<float*>(reinterpret_cast<char*>(a.cmask) + cmask_bytes(S, sum_T));
     a.xg = reinterpret_cast<uint64_t*>(handoff ? handoff : reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
-    a.arrive = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(a.xg) + xg_bytes(S, sum_T));
+    a.arrive = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.xg) + xg_bytes(S, sum_T));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a.mode = align_mode(S, mode);
     a.parts = split_parts(S, a.mode, mode);

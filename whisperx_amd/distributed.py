@@ -57,10 +57,13 @@ def _decode_dictionary(t: torch.Tensor) -> Dict[str, int]:
     return out
 
 
-def broadcast_dictionary(dictionary: Optional[Dict[str, int]], device=None, src: int = 0) -> Dict[str, int]:
+def broadcast_dictionary(dictionary: Optional[Dict[str, int]], device=None, src: int = 0,
+                         force: bool = False) -> Dict[str, int]:
     """Broadcast rank `src`'s {char: id} vocabulary to every rank (two broadcasts: shape,
-    then the packed table).  Device tensors for RCCL, CPU tensors for gloo."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    then the packed table).  Device tensors for RCCL, CPU tensors for gloo.  A world of one
+    returns a copy without a collective unless `force` (the RCCL test drives the device path
+    on a one-GPU box that way)."""
+    if not dist.is_initialized() or (dist.get_world_size() == 1 and not force):
         return dict(dictionary)
     backend = dist.get_backend()
     dev = torch.device(device) if (device is not None and backend != "gloo") else torch.device("cpu")

@@ -44,7 +44,12 @@ _TAP_BLOCK = 32  # grouped/Cin==1 convs: taps per patch block
 
 def _weight(conv: torch.nn.Conv1d) -> torch.Tensor:
     """conv.weight, with a parametrised weight (weight_norm: wav2vec2's positional conv, whose
-    re-evaluation is a 0.45 ms kernel per forward) cached until one of its originals changes."""
+    re-evaluation is a 0.45 ms kernel per forward) cached until one of its originals changes.
+
+    The cache is filled by ``materialize_weights`` on the caller's stream *before* align()
+    fans the forwards out over side streams (which wait on that stream): a weight built
+    lazily inside a side stream's first forward would be read by the other side streams
+    without any ordering against the kernels that compute it."""
     par = getattr(conv, "parametrizations", None)
     if par is None or "weight" not in par:
         return conv.weight
@@ -55,6 +60,17 @@ def _weight(conv: torch.nn.Conv1d) -> torch.Tensor:
     w = conv.weight.detach()
     conv._wx_w_cache = (key, w)
     return w
+
+
+def materialize_weights(model: torch.nn.Module) -> None:
+    """Evaluate every parametrised Conv1d weight of a prepared model on the current stream, so
+    that streams which then wait on it read a finished tensor (see _weight)."""
+    if not getattr(model, "_wx_gemm_conv", False):
+        return
+    with torch.no_grad():
+        for mod in model.modules():
+            if isinstance(mod, torch.nn.Conv1d) and hasattr(mod, "_wx_orig_forward"):
+                _weight(mod)
 
 
 def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
