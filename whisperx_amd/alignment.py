@@ -507,7 +507,8 @@ def _run_dp(ems, toks, blanks, dev):
         raise _lib.WXError(f"segment {i} ({batch.Ns[i]} tokens) uses more than {_lib.MAX_SEGMENT_COLUMNS} distinct "
                            f"emission columns and is too long for the generic forward (status 2); split it into "
                            f"shorter segments")
-    _run_dp.recovered += int(((st & _lib.STATUS_RECOVERED) != 0).sum())
+    DP_STATS["recovered_segments"] += int(((st & _lib.STATUS_RECOVERED) != 0).sum())
+    DP_STATS["segments"] += batch.S
     out = []
     for i in range(batch.S):
         a, b = batch.tok_off[i], batch.tok_off[i + 1]
@@ -515,7 +516,9 @@ def _run_dp(ems, toks, blanks, dev):
     return out
 
 
-_run_dp.recovered = 0  # segments recomputed after a lost hand-off, over the process (bench legs report it)
+# over the process: DP segments, and those recomputed in-kernel after a lost hand-off
+# (WX_STATUS_RECOVERED); the bench legs report the difference across each leg
+DP_STATS = {"segments": 0, "recovered_segments": 0}
 
 
 # ------------------------------------------------------------------ host post-processing

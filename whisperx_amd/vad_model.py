@@ -18,17 +18,25 @@ the same 5 s shape, so MIOpen tunes each convolution once) and steps 3-4 are one
 the fp32 sums are the reference's sequential ones).  The scores stay on the device:
 ``Binarize``/``merge_chunks`` read them in place (``wx_binarize``).
 
-The whisperX VAD checkpoint (``VAD_SEGMENTATION_URL``) cannot be fetched offline: ``PyanNet``
-builds the architecture with random weights, which is what the benchmarks time; a state_dict
-loads with ``load_state_dict`` (read the file with ``torch.load(..., weights_only=True)``).  Parity of the aggregation is pinned to a restatement of pyannote's
-published algorithm (oracle.vad_aggregate), not to pyannote itself, which is absent:
-"parity unpinned" at the pyannote boundary.
+The whisperX VAD checkpoint (``VAD_SEGMENTATION_URL``, pyannote/segmentation) cannot be fetched
+offline, but a local copy loads: ``PyanNet`` has pyannote's module tree and parameter names
+(``sincnet.wav_norm1d``, ``sincnet.conv1d.0.filterbank.{low_hz_,band_hz_,n_,window_}``,
+``sincnet.conv1d.{1,2}``, ``sincnet.norm1d.*``, ``lstm.*``, ``linear.*``, ``classifier``), the first
+convolution being the SincNet band-pass filterbank materialised from its learnt band edges
+(``SincFilterbank``), so ``load_vad_model(model_fp=...)`` / ``PyanNet.load_pyannote_state_dict``
+take the checkpoint's ``state_dict`` as it is.  The benchmarks time random weights.  Parity of the
+aggregation is pinned to a restatement of pyannote's published algorithm (oracle.vad_aggregate),
+not to pyannote itself, which is absent; the filterbank restates asteroid-filterbanks'
+ParamSincFB (absent too): "parity unpinned" at the pyannote boundary.
 """
 from __future__ import annotations
 
+import hashlib
 import math
+import os
 from typing import Optional
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -38,22 +46,120 @@ from .vad import SlidingWindow, SlidingWindowFeature
 SAMPLE_RATE = 16000
 
 
+def _to_mel(hz):
+    return 2595.0 * np.log10(1.0 + hz / 700.0)
+
+
+def _to_hz(mel):
+    return 700.0 * (10.0 ** (mel / 2595.0) - 1.0)
+
+
+class SincFilterbank(torch.nn.Module):
+    """SincNet's parametrised band-pass filterbank (Ravanelli & Bengio 2018, in the form of
+    asteroid-filterbanks' ParamSincFB that pyannote's SincNet uses): n_filters / 2 learnt
+    (low edge, band width) pairs in Hz, each giving a cosine-phase and a sine-phase windowed
+    band-pass filter of `kernel_size` taps (n_filters in all, cosine ones first).  Parameters
+    and buffers carry the checkpoint's names (low_hz_, band_hz_ [n/2, 1]; n_ [1, half];
+    window_ [half]).  Initialised on the mel scale between 30 Hz and sr/2 - 100 Hz."""
+
+    def __init__(self, n_filters: int = 80, kernel_size: int = 251, sample_rate: int = SAMPLE_RATE,
+                 min_low_hz: float = 50.0, min_band_hz: float = 50.0):
+        super().__init__()
+        if kernel_size % 2 == 0:
+            kernel_size += 1
+        self.n_filters, self.kernel_size, self.sample_rate = n_filters, kernel_size, sample_rate
+        self.min_low_hz, self.min_band_hz = float(min_low_hz), float(min_band_hz)
+        half = kernel_size // 2
+        mel = np.linspace(_to_mel(30.0), _to_mel(sample_rate / 2 - (min_low_hz + min_band_hz)), n_filters // 2 + 1,
+                          dtype=np.float32)
+        hz = _to_hz(mel)
+        self.low_hz_ = torch.nn.Parameter(torch.from_numpy(hz[:-1]).view(-1, 1))
+        self.band_hz_ = torch.nn.Parameter(torch.from_numpy(np.diff(hz)).view(-1, 1))
+        self.register_buffer("window_", torch.from_numpy(np.hamming(kernel_size)[:half]).float())
+        self.register_buffer("n_", 2 * math.pi * torch.arange(-half, 0.0).view(1, -1) / sample_rate)
+
+    def filters(self) -> torch.Tensor:
+        """[n_filters, 1, kernel_size]: per band, the left half of the windowed band-pass
+        impulse response (difference of the two edges' sinc kernels), its centre tap and the
+        mirrored right half, normalised by twice the band width."""
+        low = self.min_low_hz + torch.abs(self.low_hz_)
+        high = torch.clamp(low + self.min_band_hz + torch.abs(self.band_hz_), self.min_low_hz, self.sample_rate / 2)
+        band = (high - low)[:, 0]
+        ft_low = torch.matmul(low, self.n_)
+        ft_high = torch.matmul(high, self.n_)
+        out = []
+        for phase in ("cos", "sin"):
+            if phase == "cos":
+                left = ((torch.sin(ft_high) - torch.sin(ft_low)) / (self.n_ / 2)) * self.window_
+                centre = 2 * band.view(-1, 1)
+                right = torch.flip(left, dims=[1])
+            else:
+                left = ((torch.cos(ft_low) - torch.cos(ft_high)) / (self.n_ / 2)) * self.window_
+                centre = torch.zeros_like(band.view(-1, 1))
+                right = -torch.flip(left, dims=[1])
+            bp = torch.cat([left, centre, right], dim=1) / (2 * band[:, None])
+            out.append(bp.view(self.n_filters // 2, 1, self.kernel_size))
+        return torch.cat(out, dim=0)
+
+
+class SincEncoder(torch.nn.Module):
+    """The filterbank as a bias-free strided convolution (asteroid Encoder).  The filters are
+    a function of the band edges only: they are materialised once per parameter version and
+    cached (inference), not rebuilt by every forward."""
+
+    def __init__(self, stride: int = 10, **fb):
+        super().__init__()
+        self.filterbank = SincFilterbank(**fb)
+        self.stride = stride
+        self._cache = None
+
+    def weight(self) -> torch.Tensor:
+        fb = self.filterbank
+        if torch.is_grad_enabled():
+            return fb.filters()
+        key = tuple((p.data_ptr(), p._version, p.device) for p in (fb.low_hz_, fb.band_hz_))
+        if self._cache is None or self._cache[0] != key:
+            with torch.no_grad():
+                self._cache = (key, fb.filters())
+        return self._cache[1]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return F.conv1d(x, self.weight(), stride=self.stride)
+
+
+class SincNet(torch.nn.Module):
+    """pyannote's SincNet block: waveform InstanceNorm, then [sinc filterbank (|.|), conv(80->60,
+    k=5), conv(60->60, k=5)], each followed by MaxPool(3) -> InstanceNorm -> LeakyReLU."""
+
+    def __init__(self, sample_rate: int = SAMPLE_RATE, stride: int = 10):
+        super().__init__()
+        self.wav_norm1d = torch.nn.InstanceNorm1d(1, affine=True)
+        self.conv1d = torch.nn.ModuleList([SincEncoder(stride=stride, sample_rate=sample_rate),
+                                           torch.nn.Conv1d(80, 60, 5), torch.nn.Conv1d(60, 60, 5)])
+        self.pool1d = torch.nn.ModuleList([torch.nn.MaxPool1d(3, stride=3) for _ in range(3)])
+        self.norm1d = torch.nn.ModuleList([torch.nn.InstanceNorm1d(80, affine=True), torch.nn.InstanceNorm1d(60, affine=True),
+                                           torch.nn.InstanceNorm1d(60, affine=True)])
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.wav_norm1d(x)
+        for i, (conv, pool, norm) in enumerate(zip(self.conv1d, self.pool1d, self.norm1d)):
+            x = conv(x)
+            if i == 0:
+                x = torch.abs(x)
+            x = F.leaky_relu(norm(pool(x)))
+        return x
+
+
 class PyanNet(torch.nn.Module):
-    """pyannote/segmentation's PyanNet shape (pyannote.audio PyanNet / SincNet defaults):
-    waveform InstanceNorm -> [conv(1->80, k=251, s=10) |abs|, conv(80->60, k=5),
-    conv(60->60, k=5)] each followed by MaxPool(3) -> InstanceNorm -> LeakyReLU -> BiLSTM(128, 2
-    layers) -> 2 x (Linear(128) + LeakyReLU) -> Linear(n_classes) -> sigmoid.  The first conv
-    is a plain Conv1d here (SincNet's band-pass parametrisation only shapes its weights).
-    Output: [batch, frames, n_classes]; 293 frames per 5 s window (270-sample step)."""
+    """pyannote/segmentation's PyanNet (pyannote.audio PyanNet defaults, module names as in its
+    checkpoints): SincNet (stride 10) -> BiLSTM(128, 2 layers, batch-first) -> 2 x (Linear(128)
+    + LeakyReLU) -> Linear(n_classes) -> sigmoid (multi-label: whisperX's VAD checkpoint has 3
+    speaker classes).  Output: [batch, frames, n_classes]; 293 frames per 5 s window
+    (270-sample step, 991-sample receptive field)."""
 
     def __init__(self, n_classes: int = 3, lstm_hidden: int = 128, lstm_layers: int = 2, linear_hidden: int = 128):
         super().__init__()
-        self.wav_norm = torch.nn.InstanceNorm1d(1, affine=True)
-        self.conv = torch.nn.ModuleList([torch.nn.Conv1d(1, 80, 251, stride=10), torch.nn.Conv1d(80, 60, 5),
-                                         torch.nn.Conv1d(60, 60, 5)])
-        self.pool = torch.nn.MaxPool1d(3, stride=3)
-        self.norm = torch.nn.ModuleList([torch.nn.InstanceNorm1d(80, affine=True), torch.nn.InstanceNorm1d(60, affine=True),
-                                         torch.nn.InstanceNorm1d(60, affine=True)])
+        self.sincnet = SincNet()
         self.lstm = torch.nn.LSTM(60, lstm_hidden, num_layers=lstm_layers, bidirectional=True, batch_first=True)
         self.linear = torch.nn.ModuleList([torch.nn.Linear(2 * lstm_hidden, linear_hidden),
                                            torch.nn.Linear(linear_hidden, linear_hidden)])
@@ -73,16 +179,29 @@ class PyanNet(torch.nn.Module):
         return L // 3
 
     def forward(self, waveforms: torch.Tensor) -> torch.Tensor:
-        x = self.wav_norm(waveforms)
-        for i, (conv, norm) in enumerate(zip(self.conv, self.norm)):
-            x = conv(x)
-            if i == 0:
-                x = torch.abs(x)
-            x = F.leaky_relu(norm(self.pool(x)))
+        x = self.sincnet(waveforms)
         x, _ = self.lstm(x.transpose(1, 2))
         for lin in self.linear:
             x = F.leaky_relu(lin(x))
         return torch.sigmoid(self.classifier(x))
+
+    @classmethod
+    def from_pyannote_state_dict(cls, state_dict) -> "PyanNet":
+        """A PyanNet holding a pyannote/segmentation checkpoint's weights: the model's
+        ``state_dict`` (or a Lightning checkpoint dict holding one under "state_dict"), keys as
+        pyannote names them.  The class count is read from the classifier; the load is strict
+        (a missing or unexpected key raises, naming it)."""
+        sd = state_dict.get("state_dict", state_dict) if isinstance(state_dict, dict) else state_dict
+        w = sd.get("classifier.weight")
+        if w is None:
+            raise KeyError("not a pyannote PyanNet state_dict: no 'classifier.weight'")
+        m = cls(n_classes=int(w.shape[0]))
+        m.load_state_dict(sd, strict=True)
+        return m
+
+    def load_pyannote_state_dict(self, state_dict):
+        sd = state_dict.get("state_dict", state_dict) if isinstance(state_dict, dict) else state_dict
+        return self.load_state_dict(sd, strict=True)
 
 
 def closest_frame(t: float, start: float, duration: float, step: float) -> int:
@@ -144,3 +263,46 @@ class VoiceActivitySegmentation:
         n_frames = closest_frame(0.0 + self.duration + (n_chunks - 1) * self.step + 0.5 * fd, 0.0, fd, fs) + 1
         data = _lib.vad_aggregate(scores, starts, n_frames, missing=math.nan)
         return SlidingWindowFeature(data[:, None], SlidingWindow(start=0.0, duration=fd, step=fs))
+
+    def instantiate(self, hyperparameters: dict) -> "VoiceActivitySegmentation":
+        """pyannote Pipeline.instantiate: keeps the binarisation hyper-parameters (onset,
+        offset, min_duration_on/off), which transcribe passes to merge_chunks separately."""
+        self.hyperparameters = dict(hyperparameters)
+        return self
+
+
+VAD_SEGMENTATION_URL = ("https://whisperx.s3.eu-west-2.amazonaws.com/model_weights/segmentation/"
+                        "0b5b3216d60a2d32fc086b47ea8c67589aaeb26b7e07fcbe620d6d0b83e209ea/pytorch_model.bin")
+
+
+def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=None, model_fp=None,
+                   check_sha256: bool = True) -> VoiceActivitySegmentation:
+    """vad.py:20-59 without the download: the segmentation checkpoint at `model_fp` (default:
+    torch hub's whisperx-vad-segmentation.bin, where the reference caches its download) is
+    checked against the SHA256 in VAD_SEGMENTATION_URL like the reference does
+    (`check_sha256=False` for a checkpoint of one's own), read with
+    ``torch.load(..., weights_only=True)`` (nothing in the file is executed) and loaded into a
+    PyanNet; returns the producer pipeline with the reference's hyper-parameters.  A file that
+    is absent raises (offline: there is nothing to fetch it from)."""
+    if model_fp is None:
+        model_fp = os.path.join(torch.hub._get_torch_home(), "whisperx-vad-segmentation.bin")
+    if os.path.exists(model_fp) and not os.path.isfile(model_fp):
+        raise RuntimeError(f"{model_fp} exists and is not a regular file")
+    if not os.path.isfile(model_fp):
+        raise FileNotFoundError(f"{model_fp}: no VAD segmentation checkpoint (whisperx_amd does not download; "
+                                f"place the file from {VAD_SEGMENTATION_URL} there or pass model_fp)")
+    if check_sha256:
+        with open(model_fp, "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+        if digest != VAD_SEGMENTATION_URL.split("/")[-2]:
+            raise RuntimeError("Model has been downloaded but the SHA256 checksum does not not match. "
+                               "Please retry loading the model.")
+    try:
+        ckpt = torch.load(model_fp, map_location="cpu", weights_only=True)
+    except Exception as e:  # a Lightning checkpoint with pickled non-tensor objects
+        raise RuntimeError(f"{model_fp}: torch.load(weights_only=True) refused the file ({e}); save its "
+                           f"'state_dict' entry on its own and pass that file") from e
+    model = PyanNet.from_pyannote_state_dict(ckpt)
+    pipeline = VoiceActivitySegmentation(segmentation=model, device=torch.device(device))
+    return pipeline.instantiate({"onset": vad_onset, "offset": vad_offset, "min_duration_on": 0.1,
+                                 "min_duration_off": 0.1})
