@@ -185,13 +185,14 @@ def e2e_align(device, n_seg=16, seed=7):
     audio = torch.from_numpy(rng.standard_normal(int(30 * n_seg * 16000)).astype(np.float32) * 0.1)
     whisperx_amd.align([dict(s) for s in segs[:2]], model, meta, audio, device)  # warm-up
     torch.cuda.synchronize()
+    st0 = _dp_stats()
     t0 = time.perf_counter()
     out = whisperx_amd.align([dict(s) for s in segs], model, meta, audio, device)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     n_words = len(out["word_segments"])
     return {"value": 30.0 * n_seg / dt, "unit": "audio-sec/s", "segments": n_seg, "words": n_words,
-            "ms_per_segment": 1000 * dt / n_seg,
+            "ms_per_segment": 1000 * dt / n_seg, "dp": _recovered_since(st0),
             "note": "align() incl. random-weight wav2vec2-base fp32 forward per segment on the GPU "
                     "(8 HIP streams, one unpadded forward per segment)"}
 
@@ -232,12 +233,13 @@ def e2e_config3(device, seed=3):
         n_words = max(1, int((c["end"] - c["start"]) * 14 / 5.5))
         words = ["".join(rng.choice(list(letters), int(rng.integers(2, 9)))) for _ in range(n_words)]
         segs.append({"start": round(c["start"], 3), "end": round(c["end"], 3), "text": " ".join(words)})
+    st0 = _dp_stats()
     t2 = time.perf_counter()
     out = whisperx_amd.align(segs, model, meta, audio, device)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     speech = sum(c["end"] - c["start"] for c in chunks)
-    return {"audio_sec": 3600.0, "chunks": len(chunks), "speech_sec": speech,
+    return {"audio_sec": 3600.0, "chunks": len(chunks), "speech_sec": speech, "dp": _recovered_since(st0),
             "vad_merge_chunks_ms": 1000 * (t1 - t0), "align_ms": 1000 * (t3 - t2),
             "audio_sec_per_s": 3600.0 / ((t1 - t0) + (t3 - t2)),
             "words": len(out["word_segments"]),
@@ -268,6 +270,52 @@ def vad_producer_1h(device, seed=5, batch_size=2048):
             "producer_ms": 1000 * (t1 - t0), "audio_sec_per_s": 3600.0 / (t1 - t0), "batch_size": batch_size,
             "note": "PyanNet-shaped random-weight segmentation forward (fp32, 5 s windows every 0.5 s) + "
                     "wx_vad_aggregate; scores left on the device for merge_chunks; audio resident on the GPU"}
+
+
+def e2e_config3_waveform(device, seed=6):
+    """BASELINE config 3 from the waveform: 1 h of audio -> VAD producer (PyanNet-shaped
+    random-weight segmentation model + wx_vad_aggregate, vad.py:198-240) -> merge_chunks on the
+    device-resident scores (GPU Binarize, 30 s, asr.py:186-192) -> chunk bounds rounded
+    (asr.py:226-232) -> align() (random-weight wav2vec2-base forward per chunk + fused DP).
+    A random-weight segmentation model's scores hover around one value, so the hysteresis
+    thresholds are put at their median (onset = offset) to get a realistic number of chunks;
+    timings only.  The synthetic transcripts are made outside the clock."""
+    import whisperx_amd
+    from whisperx_amd import synthetic
+    from whisperx_amd.vad import merge_chunks
+    from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+    torch.manual_seed(seed)
+    vad = VoiceActivitySegmentation(device=device, batch_size=2048)
+    model = _w2v_base(device, seed)
+    meta = {"language": "en", "dictionary": synthetic.w2v_dictionary(), "type": "huggingface"}
+    g = torch.Generator().manual_seed(seed)
+    wav = (torch.randn(1, 3600 * 16000, generator=g) * 0.1).to(device)
+    tr = synthetic.Transcriber(seed)
+    # warm-up outside the clock: producer (MIOpen, LSTM), Binarize, align
+    feat = vad({"waveform": wav[:, : 120 * 16000], "sample_rate": 16000})
+    thr = float(torch.nanmedian(feat.data).item())
+    merge_chunks(feat, 30, thr, thr)
+    whisperx_amd.align(tr.segments([{"start": 0.0, "end": 30.0}]), model, meta, wav[0, : 60 * 16000], device)
+    torch.cuda.synchronize()
+    st0 = _dp_stats()
+    t0 = time.perf_counter()
+    feat = vad({"waveform": wav, "sample_rate": 16000})
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    chunks = merge_chunks(feat, 30, thr, thr)
+    t2 = time.perf_counter()
+    segs = tr.segments(chunks)
+    t3 = time.perf_counter()
+    out = whisperx_amd.align(segs, model, meta, wav[0], device)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    wall = (t1 - t0) + (t2 - t1) + (t4 - t3)
+    return {"audio_sec": 3600.0, "chunks": len(chunks), "producer_ms": 1000 * (t1 - t0),
+            "merge_chunks_ms": 1000 * (t2 - t1), "align_ms": 1000 * (t4 - t3), "audio_sec_per_s": 3600.0 / wall,
+            "words": len(out["word_segments"]), "dp": _recovered_since(st0), "threshold": thr,
+            "note": "waveform -> VAD producer -> GPU merge_chunks -> align() incl. per-chunk wav2vec2-base fp32 "
+                    "forward; random weights (thresholds at the scores' median), synthetic audio/transcripts"}
 
 
 def _w2v_base(device, seed):
@@ -308,6 +356,7 @@ def corpus_config4(device, rank, world, dist_on, seed=4):
     torch.cuda.synchronize()
     if dist_on:
         torch.distributed.barrier()
+    st0 = _dp_stats()
     t0 = time.perf_counter()
     n_seg, n_words = 0, 0
     for i, scores, audio in files:
@@ -325,7 +374,10 @@ def corpus_config4(device, rank, world, dist_on, seed=4):
     else:
         el_max, n_seg_all, n_words_all, n_files = el, n_seg, n_words, len(mine)
     total = float(sum(durs))
-    return {"files": int(n_files), "audio_sec": total, "n_gpus": world, "segments": int(n_seg_all),
+    rec = _recovered_since(st0)
+    if dist_on:
+        rec = dict(zip(rec, (int(x) for x in _allreduce(list(rec.values()), "sum"))))
+    return {"files": int(n_files), "audio_sec": total, "n_gpus": world, "segments": int(n_seg_all), "dp": rec,
             "words": int(n_words_all), "wall_s": el_max, "audio_sec_per_s": total / el_max,
             "segments_per_s": n_seg_all / el_max, "scaling": "strong (fixed 10 h corpus)",
             "shard": "LPT by duration (distributed.shard_files)",
@@ -333,7 +385,7 @@ def corpus_config4(device, rank, world, dist_on, seed=4):
                     "forward per chunk; synthetic VAD scores/audio/transcripts resident before the clock"}
 
 
-def _cpu_reference_align(segs, model_cpu, dictionary, audio):
+def _cpu_reference_align(segs, model_cpu, dictionary, audio, lang="en", chars=False):
     """The reference's CPU align() path (device='cpu'): CPU forward + log_softmax per segment
     (alignment.py:209-235), the DP on the CPU (oracle TorchPort: get_trellis / backtrack /
     merge_repeats with the reference's per-timestep torch ops, :359-454), then the host
@@ -348,7 +400,7 @@ def _cpu_reference_align(segs, model_cpu, dictionary, audio):
     out = []
     for seg in segs:
         seg = dict(seg)
-        A._prepare(seg, dictionary, "en")
+        A._prepare(seg, dictionary, lang)
         tokens = [dictionary[c] for c in "".join(seg["clean_char"])]
         wav = audio[:, int(seg["start"] * 16000): int(seg["end"] * 16000)]
         t0 = time.perf_counter()
@@ -361,7 +413,7 @@ def _cpu_reference_align(segs, model_cpu, dictionary, audio):
             ss = np.array([m[1] for m in merged])
             se = np.array([m[2] for m in merged])
             sc = np.array([m[3] for m in merged])
-            out += A.aggregate_segment(seg, ss, se, sc, em.shape[0], 1, "en", "nearest", False)
+            out += A.aggregate_segment(seg, ss, se, sc, em.shape[0], 1, lang, "nearest", chars)
         t3 = time.perf_counter()
         t_fwd, t_dp, t_agg = t_fwd + t1 - t0, t_dp + t2 - t1, t_agg + t3 - t2
     return out, (t_fwd, t_dp, t_agg)
@@ -404,22 +456,43 @@ def cpu_align_baseline(threads, budget_s=20.0, seed=11):
             "aggregate_ms": 1000 * tot[2] / n}
 
 
-def mae_e2e(device, n_seg=4, seed=7):
-    """north_star parity on the real emission path: the same random-weight wav2vec2-base and
-    the same audio through (a) align() on the GPU (GPU forward + fused HIP DP) and (b) the
-    reference's CPU path (CPU forward + CPU DP).  Word start/end MAE in ms and the number of
-    segments whose char token paths differ."""
+def _w2v_large(device, seed, V=40):
+    """Random-weight wav2vec2-large-xlsr-shaped CTC model (BASELINE config 5 / the layer-norm
+    family of the HF default alignment models, alignment.py:32-61): 24 layers of 1024, layer-norm
+    feature encoder with conv bias, stable layer norm."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    torch.manual_seed(seed)
+    cfg = Wav2Vec2Config(vocab_size=V, hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                         intermediate_size=4096, feat_extract_norm="layer", do_stable_layer_norm=True,
+                         conv_bias=True)
+    return Wav2Vec2ForCTC(cfg).to(device).eval()
+
+
+def mae_e2e(device, n_seg=4, seed=7, large=False, seg_s=30.0):
+    """north_star parity on the real emission path: the same random-weight wav2vec2 and the
+    same audio through (a) align() on the GPU (GPU forward + fused HIP DP) and (b) the
+    reference's CPU path (CPU forward + CPU DP).  Word start/end MAE in ms, and the segments
+    whose char (token path) times differ.  large=True: config 5 (wav2vec2-large-xlsr shape,
+    V = 40 German characters, 60 s segments)."""
     import whisperx_amd
     from whisperx_amd import synthetic
 
-    model = _w2v_base(device, seed)
-    model_cpu = _w2v_base("cpu", seed)
-    segs, audio = _e2e_inputs(n_seg, seed)
-    dictionary = synthetic.w2v_dictionary()
-    meta = {"language": "en", "dictionary": dictionary, "type": "huggingface"}
-    gpu = whisperx_amd.align([dict(s) for s in segs], model, meta, audio, device)["segments"]
-    cpu, _ = _cpu_reference_align(segs, model_cpu, dictionary, audio[None])
-    errs, n_words, n_diff = [], 0, 0
+    if large:
+        model, model_cpu = _w2v_large(device, seed), _w2v_large("cpu", seed)
+        dictionary, letters, lang = synthetic.de_dictionary(), synthetic.DE_LETTERS, "de"
+    else:
+        model, model_cpu = _w2v_base(device, seed), _w2v_base("cpu", seed)
+        dictionary, letters, lang = synthetic.w2v_dictionary(), synthetic.LETTERS, "en"
+    tr = synthetic.Transcriber(seed, letters=letters)
+    segs = tr.segments([{"start": seg_s * k, "end": seg_s * (k + 1)} for k in range(n_seg)])
+    g = torch.Generator().manual_seed(seed)
+    audio = torch.randn(int(seg_s * n_seg * 16000), generator=g) * 0.1
+    meta = {"language": lang, "dictionary": dictionary, "type": "huggingface"}
+    gpu = whisperx_amd.align([dict(s) for s in segs], model, meta, audio, device,
+                             return_char_alignments=True)["segments"]
+    cpu, _ = _cpu_reference_align(segs, model_cpu, dictionary, audio[None], lang=lang, chars=True)
+    errs, n_words, n_diff, n_path = [], 0, 0, 0
     for a, b in zip(gpu, cpu):
         wa, wb = a["words"], b["words"]
         seg_diff = False
@@ -430,9 +503,31 @@ def mae_e2e(device, n_seg=4, seed=7):
                     seg_diff |= x[k] != y[k]
             n_words += 1
         n_diff += int(seg_diff or len(wa) != len(wb))
+        ca = [(c.get("start"), c.get("end")) for c in a.get("chars", [])]
+        cb = [(c.get("start"), c.get("end")) for c in b.get("chars", [])]
+        n_path += int(ca != cb)
+    del model, model_cpu
+    torch.cuda.empty_cache()
     return {"mae_ms": float(np.mean(errs)) if errs else None, "max_ms": float(np.max(errs)) if errs else None,
             "words": n_words, "segments": len(gpu), "segments_with_differing_times": n_diff,
-            "frame_ms": 20.0, "vs": "reference CPU align() path (CPU forward + CPU DP), same weights and audio"}
+            "segments_with_differing_token_paths": n_path, "frame_ms": 1000.0 * seg_s / ((seg_s * 16000 - 400) // 320 + 1),
+            "model": ("wav2vec2-large-xlsr shape (24 x 1024, layer-norm feature encoder), V=40 DE, "
+                      f"{n_seg} x {seg_s:.0f} s" if large else f"wav2vec2-base shape, V=32 EN, {n_seg} x {seg_s:.0f} s"),
+            "vs": "reference CPU align() path (CPU forward + CPU DP), same weights and audio"}
+
+
+def _recovered_since(before):
+    """Segments the legs' align() calls recomputed in-kernel after a lost split hand-off
+    (WX_STATUS_RECOVERED), since `before` (a copy of alignment.DP_STATS)."""
+    from whisperx_amd import alignment
+
+    return {k: alignment.DP_STATS[k] - before[k] for k in before}
+
+
+def _dp_stats():
+    from whisperx_amd import alignment
+
+    return dict(alignment.DP_STATS)
 
 
 def _allreduce(vals, op):
@@ -556,6 +651,7 @@ def main():
                                             f" (+{len(knames) - 1} more launches)"),
                          "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6},
         }
+        out["roofline"]["dp"] = _lib.status_summary(plan.status[: batch.S])
         mae, ntok, nbad = mae_vs_oracle([e.cpu().numpy() for e in ems], toks, plan)
         out["mae_ms"] = mae
         out["mae_detail"] = {"tokens": ntok, "segments_with_path_mismatch": nbad, "vs": "CPU oracle, same emission"}
@@ -577,7 +673,8 @@ def main():
                                   "audio_sec_per_s": sum(b2.Ts) * FRAME_S / (d2 / 5),
                                   "achieved_GBps": B2 / (d2 / 5) / 1e9,
                                   "frac": B2 / (d2 / 5) / 1e9 / HBM_PEAK_GBPS,
-                                  "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b2.Ts, b2.Ns))) / (d2 / 5)}
+                                  "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b2.Ts, b2.Ns))) / (d2 / 5),
+                                  "dp": _lib.status_summary(p2.status[: b2.S])}
             del p2, b2
             torch.cuda.empty_cache()
             # the north star's roofline case: T=3000 x V=32 trellises (N ~ 900, 60 s segments)
@@ -594,7 +691,8 @@ def main():
                                         "audio_sec_per_s": sum(b3.Ts) * FRAME_S / (d3 / 3),
                                         "achieved_GBps": B3 / (d3 / 3) / 1e9,
                                         "frac": B3 / (d3 / 3) / 1e9 / HBM_PEAK_GBPS,
-                                        "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b3.Ts, b3.Ns))) / (d3 / 3)}
+                                        "cells_per_s": float(sum(t_ * n_ for t_, n_ in zip(b3.Ts, b3.Ns))) / (d3 / 3),
+                                        "dp": _lib.status_summary(p3.status[: b3.S])}
             # get_trellis (materialised, wx_trellis) on the same T=3000 batch: the HBM-write-bound
             # kernel of the path (4 B per cell written)
             try:
@@ -658,6 +756,10 @@ def main():
                 extra["e2e_config3_1h"] = e2e_config3(device)
             except Exception as e:
                 extra["e2e_config3_1h"] = {"error": repr(e)[:200]}
+            try:
+                extra["e2e_config3_1h_from_waveform"] = e2e_config3_waveform(device)
+            except Exception as e:
+                extra["e2e_config3_1h_from_waveform"] = {"error": repr(e)[:300]}
             log("bench: emission-path MAE ...")
             try:
                 me = mae_e2e(device)
@@ -665,6 +767,12 @@ def main():
                 extra["mae_e2e"] = me
             except Exception as e:
                 extra["mae_e2e"] = {"error": repr(e)[:300]}
+            try:  # config 5: the layer-norm (large-xlsr) family, V = 40, 60 s segments
+                m5 = mae_e2e(device, n_seg=2, seed=5, large=True, seg_s=60.0)
+                out["mae_e2e_cfg5_ms"] = m5["mae_ms"]
+                extra["mae_e2e_cfg5"] = m5
+            except Exception as e:
+                extra["mae_e2e_cfg5"] = {"error": repr(e)[:300]}
             ca = extra.get("cpu_align_config1", {}).get("all_threads", {})
             ea = extra.get("e2e_align", {})
             if "value" in ca and "value" in ea:

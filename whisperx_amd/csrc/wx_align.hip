@@ -207,6 +207,43 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, i
     }
 }
 
+// Quad-interleaved staging (the register-resident forward, Forward::kReg).  A chunk's 32 rows
+// are kept as 8 row quads; quad p holds, per column c, the 4 values em[4p..4p+3, c] in 16
+// contiguous bytes: float index p * QS + 4 c + (row & 3), QS = 4 (VS + 1).  One 16-byte LDS
+// read then gives a lane 4 steps of its token's column (and, read at a uniform address, 4
+// steps of the blank), instead of one or two dwords per step.  Column VS of each quad is not
+// staged: the column-0 helper writes the column-1 wave's lane-0 operand there (see
+// Forward::col0_pre).  LDS-DMA writes lane-linear: one dword per lane, lane i carrying row
+// 4p + (i & 3), column 16h + (i >> 2) of half h, lands exactly at p * QS + 64 h + i.
+template <int VS>
+__host__ __device__ constexpr int quad_stride() { return 4 * (VS + 1); }
+template <int VS>
+__host__ __device__ constexpr int quad_buf_floats() { return 8 * quad_stride<VS>(); }
+
+template <int VS>
+__device__ __forceinline__ void stage_quads(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
+    const int l = lane_id();
+    const unsigned base = (unsigned)uniform((int)lds_addr(dst));
+    const int r = l & 3;
+#pragma unroll
+    for (int p = 0; p < kChunk / 4; ++p) {
+        if (4 * p >= nrows) break;  // (uniform)
+#pragma unroll
+        for (int h = 0; h < VS / 16; ++h) {
+            const int c = 16 * h + (l >> 2);
+            if (c < V && 4 * p + r < nrows)
+                glds_dword(E + (int64_t)(r0 + 4 * p) * V, (unsigned)(r * V + c) * 4u,
+                           base + (unsigned)((p * quad_stride<VS>() + 64 * h) * 4));
+        }
+    }
+}
+// LDS-DMA instructions stage_quads issues for a chunk of `nrows` rows (the helper's vmcnt: a
+// half whose every lane is masked, 16 h >= V, is branched over and never issued)
+template <int VS>
+__device__ __forceinline__ int quad_loads(int nrows, int V) {
+    return nrows <= 0 ? 0 : ((nrows + 3) / 4) * min(VS / 16, (V + 15) / 16);
+}
+
 // The column map of one segment (all threads of the workgroup): columns 0 and `blank` and
 // every token id (ids outside [0, V) count as 0, as the DP reads them).  Returns the compact
 // width, uniform; > kGatherVS means the segment cannot be staged.
@@ -259,6 +296,19 @@ __device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, i
 }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// s_waitcnt vmcnt with a (uniform) runtime count: waits until at most the largest of a few
+// immediates <= n of this wave's vector-memory operations are outstanding (over-waiting is
+// always correct: a smaller count only waits for more).
+__device__ __forceinline__ void wait_vm_le(int n) {
+    if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 __device__ __forceinline__ void wave_fence() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -432,6 +482,18 @@ struct Forward {
     // loads; a multiple of 4: column-N history is stored as float4).
     static constexpr int kU = C >= 8 ? WX_C8_UNROLL : kUnroll;
     static_assert(!(H && MODE == 1), "the materialising kernel computes column 0 in wave 0");
+    // Register-resident chunks (split kernels with one cell per lane, the latency shape of
+    // config 2): a chunk's operands are read into registers during the previous chunk (16-byte
+    // reads of quad-interleaved rows), so the 32 steps of a chunk are a pure VALU chain — no
+    // LDS read, no wait.  Micro-benchmarks (tools/ubench/step*.hip): a step costs ~20 cycles
+    // of one wave alone, each LDS read issued inside the chain ~9 more.
+#ifndef WX_NO_REG_CHUNK
+    static constexpr bool kReg = C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS;
+#else
+    static constexpr bool kReg = false;
+#endif
+    static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
+    static constexpr int kQS = quad_stride<VS>();
 
     // Per-lane state of the forward pass.
     struct State {
@@ -479,7 +541,7 @@ struct Forward {
                                                float* __restrict__ q0,        // MODE 0: exp(em[t,0]) per row
                                                float* __restrict__ cn,        // MODE 0: column N of rows 1..T
                                                float* __restrict__ tr,        // MODE 1: trellis
-                                               float* lds /* kBufs * kChunk * VS */,
+                                               float* lds /* kBufs * kBufFloats */,
                                                float* c0b /* H: 2 * kChunk column-0 values */,
                                                float* xh /* 2 * W * 64: chunk halo copies */, bool x4,
                                                const ColMap& cm /* VS == kGatherVS: column map */,
@@ -494,7 +556,13 @@ struct Forward {
             // NH == 2 (split kernels): wave W stages, wave W + 1 runs column 0's fp64 chain;
             // one helper doing both paced part 0 (it reached every chunk barrier last)
             const bool col0 = (!SP || sp->p == 0) && (NH == 1 || wv == W + 1);
-            helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
+            if constexpr (kReg) {
+                int t0 = N > 0 ? tok[d.tok0] : 0;
+                t0 = (t0 >= 0 && t0 < V) ? t0 : 0;
+                helper_reg(d, E, V, lds, nch, t0, col0, wv == W);
+            } else {
+                helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
+            }
             return false;
         }
         const int l = lane_id();
@@ -507,12 +575,13 @@ struct Forward {
             // no column of this wave exists: keep the barrier count (and, without a helper,
             // this wave's share of the staging)
             if (!H && nch > 0) stage_rows<VS, W>(E, V, 0, min(kChunk, T), lds, x4, cm);
+            if (kReg) __syncthreads();  // (the register-resident protocol's barrier -1)
             for (int q = 0; q < nch; ++q) {
                 wait_vm();
                 __syncthreads();
                 if (!H && q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
-                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4, cm);
+                                      lds + ((q + 1) % kBufs) * kBufFloats, x4, cm);
             }
             return false;
         }
@@ -595,9 +664,15 @@ struct Forward {
 #pragma unroll
             for (int k = 0; k < C; ++k) bits[((int64_t)qd * C + k) * lanes + g] = wdef[k];
         };
-        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C]) {
+        // kReg: the operands of the chunk being computed (o) and of the next one (n), swapped
+        // by the two-way unrolled chunk loop
+        RegOps opsA, opsB;
+        const int etq = (vw == 0 && l == 0) ? VS * 16 : toff[0] * 4;  // quad byte offset of this lane's column
+        const int ebq = boff * 4;                                      // ... of the blank (uniform)
+        if (kReg) __syncthreads();  // barrier -1 (helper_reg: the column-0 helper's first two chunks)
+        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C], RegOps& o, RegOps& n) {
             WX_T(c0);
-            float* buf = lds + (q % kBufs) * kChunk * VS;
+            float* buf = lds + (q % kBufs) * kBufFloats;
             const int rows = min(kChunk, T - q * kChunk);
             float* xq = xh + (q & 1) * W * kWave;
             if (W > 1 && q > 0 && wv < W - 1 && l >= kWave - Geo::HL) {  // publish this chunk's halo
@@ -655,16 +730,25 @@ struct Forward {
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
-                                      lds + ((q + 1) % kBufs) * kChunk * VS, x4, cm);
+                                      lds + ((q + 1) % kBufs) * kBufFloats, x4, cm);
                 if (MODE == 0 && wv == 0 && l < rows) q0[q * kChunk + l] = exp_cr(buf[l * VS]);  // never idle
             }
             const char* bb = reinterpret_cast<const char*>(buf);
             const float* c0q = H ? c0b + (q & 1) * kChunk : nullptr;
             WX_T(c3);
-            if (vw == 0)
+            if constexpr (kReg) {
+                if (q == 0) reg_load(o, bb, etq, ebq);
+                // the next chunk's operands (the last chunk re-reads its own rows: harmless)
+                const char* nb = reinterpret_cast<const char*>(lds + ((q + 1 < nch ? q + 1 : q) % kBufs) * kBufFloats);
+                float cur0 = st.cur[0];
+                reg_chunk(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T);
+                st.cur[0] = cur0;
+                st.t += rows;
+            } else if (vw == 0) {
                 chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
-            else
+            } else {
                 chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+            }
             WX_T(c4);
 #ifdef WX_PHASE_TIMING
             acc_steps += c4 - c3;
@@ -675,7 +759,10 @@ struct Forward {
                 const int sh = kChunk - rows;  // keep bit 31 = first step of the block
 #pragma unroll
                 for (int k = 0; k < C; ++k) {
-                    const unsigned wq = (sh == 0) ? st.w[k] : (st.w[k] << sh);
+                    // (kReg runs all 32 steps of a partial chunk: bit 31 is already the first
+                    // step, the bits of the steps past T are dropped)
+                    const unsigned wq = kReg ? (st.w[k] & (0xFFFFFFFFu << sh))
+                                             : ((sh == 0) ? st.w[k] : (st.w[k] << sh));
                     if (SP)
                         wdef[k] = wq;
                     else if (!halo && g < L.G)  // (lanes past column N: words the walk never reads)
@@ -686,12 +773,12 @@ struct Forward {
         };
         if constexpr (SP) {
             for (int q = 0; q < nch; q += 2) {
-                chunk_iter(q, xeven);
-                if (q + 1 < nch) chunk_iter(q + 1, xodd);
+                chunk_iter(q, xeven, opsA, opsB);
+                if (q + 1 < nch) chunk_iter(q + 1, xodd, opsB, opsA);
             }
             if (MODE == 0 && nch > 0 && !halo && g < L.G) store_deferred(nch - 1);
         } else {
-            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven);
+            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB);
         }
 #ifdef WX_PHASE_TIMING
         if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
@@ -710,6 +797,136 @@ struct Forward {
         return xlost;
     }
 
+    // ---------------------------------------------------------------- register-resident chunks
+    struct RegOps {
+        float4 et[kChunk / 4];  // em[t, tok] of this lane's cell (column-1 wave, lane 0: col0_pre's value)
+        float4 eb[kChunk / 4];  // em[t, blank]
+    };
+    __device__ __forceinline__ static void reg_load(RegOps& o, const char* buf, int etq, int ebq) {
+#pragma unroll
+        for (int p = 0; p < kChunk / 4; ++p) {
+            o.et[p] = *reinterpret_cast<const float4*>(buf + p * kQS * 4 + etq);
+            o.eb[p] = *reinterpret_cast<const float4*>(buf + p * kQS * 4 + ebq);
+        }
+    }
+    __device__ __forceinline__ static float comp(const float4& v, int j) {
+        return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+    }
+    // Four time steps of one cell (alignment.py:372-378), hand-ordered so that the chain
+    // through the cell value (maximum -> next step's DPP add) needs no wait states: the DPP's
+    // source is read two instructions after the maximum that wrote it (the addc and the stay
+    // add sit in between).  One asm block per four steps: hipcc cannot see inside a block and
+    // pads an s_nop at every block boundary whose next block might read a fresh VGPR through
+    // DPP.  Lane 0's left input is zero-filled: in the column-1 wave its operand `et` is
+    // col0_pre's tr[t][0] + em[t, tok[0]] (0 + x is x for every x the DP can tell apart: it
+    // only compares values and takes maxima), elsewhere a halo lane's don't-care.  n[k] =
+    // the cell value after step k.
+#define WX_REG_STEP(CUR, NC, ET, EB)                                                                  \
+    "v_add_f32 %[s], %[" #CUR "], %[" #EB "]\n\t"                                                   \
+    "v_add_f32_dpp %[c], %[" #CUR "], %[" #ET "] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t" \
+    "v_cmp_gt_f32 vcc, %[c], %[s]\n\t"                                                              \
+    "v_maximum3_f32 %[" #NC "], %[s], %[c], %[c]\n\t"                                               \
+    "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc\n\t"
+    __device__ __forceinline__ static void reg_steps4(float cur, unsigned& w, const float4& et, const float4& eb,
+                                                      float (&n)[4]) {
+        float s, c;
+        asm volatile(WX_REG_STEP(cur, n0, e0, b0) WX_REG_STEP(n0, n1, e1, b1) WX_REG_STEP(n1, n2, e2, b2)
+                         WX_REG_STEP(n2, n3, e3, b3)
+                     : [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3]), [w] "+v"(w),
+                       [s] "=&v"(s), [c] "=&v"(c)
+                     : [cur] "v"(cur), [e0] "v"(et.x), [e1] "v"(et.y), [e2] "v"(et.z), [e3] "v"(et.w),
+                       [b0] "v"(eb.x), [b1] "v"(eb.y), [b2] "v"(eb.z), [b3] "v"(eb.w)
+                     : "vcc");
+    }
+#undef WX_REG_STEP
+    // 32 steps on operands `o`, issuing the next chunk's operand reads (n, from buffer nb) one
+    // quad ahead of each group of four steps; column N history stored by the owner lane (rows
+    // past T skipped: the steps of a partial chunk past T compute on stale rows, harmlessly).
+    __device__ __forceinline__ static void reg_chunk(const RegOps& o, RegOps& n, const char* nb, int etq, int ebq,
+                                                     float& cur, unsigned& w, bool owner, float* __restrict__ cn,
+                                                     int t0, int T) {
+        float hist[8];
+        // the first DPP may read a value a VALU op just wrote (halo copy-in): two wait states
+        asm volatile("s_nop 1");
+#pragma unroll
+        for (int p = 0; p < kChunk / 4; ++p) {
+            n.et[p] = *reinterpret_cast<const float4*>(nb + p * kQS * 4 + etq);
+            n.eb[p] = *reinterpret_cast<const float4*>(nb + p * kQS * 4 + ebq);
+            __builtin_amdgcn_sched_barrier(0);
+            float nv[4];
+            reg_steps4(cur, w, o.et[p], o.eb[p], nv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hist[(4 * p + j) & 7] = nv[j];
+            cur = nv[3];
+            if ((p & 1) && owner) {  // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7]
+                const int tb = t0 + 8 * (p >> 1);
+                if (tb + 8 <= T) {
+                    float4* d4 = reinterpret_cast<float4*>(cn + tb);
+                    d4[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
+                    d4[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (tb + k < T) cn[tb + k] = hist[k];
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // tr[t][0] + em[t, tok[0]] for the rows of chunk q (the column-1 wave's lane-0 operand),
+    // into column VS of the chunk's quad buffer.  tr[t][0] (alignment.py:367-370): 0 at t = 0,
+    // fp32 of the fp64 sum of em[0..t-1, 0] (torch CPU cumsum accumulates in double), +inf in
+    // the last N rows.  The fp64 chain runs on wave-uniform values (16-byte broadcast reads).
+    __device__ __forceinline__ static void col0_pre(int q, const SegDesc& d, float* buf, int tok0, double& acc) {
+        const int T = d.T, N = d.N;
+        float4 e0[kChunk / 4], et[kChunk / 4];
+#pragma unroll
+        for (int p = 0; p < kChunk / 4; ++p) {
+            e0[p] = *reinterpret_cast<const float4*>(buf + p * kQS);
+            et[p] = *reinterpret_cast<const float4*>(buf + p * kQS + 4 * tok0);
+        }
+#pragma unroll
+        for (int p = 0; p < kChunk / 4; ++p) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = q * kChunk + 4 * p + j;
+                v[j] = col0_value(t, acc, T, N) + comp(et[p], j);
+                acc += (double)comp(e0[p], j);
+            }
+            if (lane_id() == 0) *reinterpret_cast<float4*>(buf + p * kQS + 4 * VS) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+    // The two helpers of a register-resident split kernel.  Barriers: -1, then one per chunk.
+    // Wave W stages quads four chunks ahead and makes chunks <= q + 2 land before barrier q;
+    // wave W + 1 (part 0 only) writes col0_pre of chunks 0 and 1 after barrier -1 and of chunk
+    // q + 2 after barrier q.  So after barrier q the DP waves can read chunk q + 1's operands,
+    // col0_pre included, while they compute chunk q; buffer q % 4 is restaged with chunk q + 4
+    // after barrier q (its rows were read during chunk q - 1, its col0_pre during chunk q - 2).
+    __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, int nch,
+                                      int tok0, bool col0, bool stage) {
+        const int T = d.T;
+        auto buf = [&](int q) { return lds + (q % kBufs) * kBufFloats; };
+        auto rows_of = [&](int q) { return (q >= 0 && q < nch) ? min(kChunk, T - q * kChunk) : 0; };
+        auto loads = [&](int q) { return quad_loads<VS>(rows_of(q), V); };
+        if (stage) {
+            for (int i = 0; i < 4 && i < nch; ++i) stage_quads<VS>(E, V, i * kChunk, rows_of(i), buf(i));
+            wait_vm_le(loads(2) + loads(3));  // barrier -1 needs chunks 0 and 1
+        }
+        double acc = 0.0;
+        __syncthreads();  // barrier -1
+        if (col0) {
+            col0_pre(0, d, buf(0), tok0, acc);
+            if (nch > 1) col0_pre(1, d, buf(1), tok0, acc);
+        }
+        for (int q = 0; q < nch; ++q) {
+            if (stage) wait_vm_le(loads(q + 3));  // chunks <= q + 2 landed
+            __syncthreads();                      // barrier q
+            if (stage && q + 4 < nch) stage_quads<VS>(E, V, (q + 4) * kChunk, rows_of(q + 4), buf(q + 4));
+            if (col0 && q + 2 < nch) col0_pre(q + 2, d, buf(q + 2), tok0, acc);
+        }
+    }
+
     // The helper wave (H): mirrors the DP waves' barriers.  Before barrier q, chunks q and
     // q+1 are staged and column 0 of chunk q is in c0b[q & 1].  (q0 is filled after the
     // forward pass, while wave 0 walks: fill_q0.)
@@ -724,7 +941,7 @@ struct Forward {
         // count: 4 for 16-byte staging, 32 for row staging; gathers drain fully).
         if (stage) {
             for (int i = 0; i < 3 && i < nch; ++i)
-                stage_rows<VS, 1, true>(E, V, i * kChunk, min(kChunk, T - i * kChunk), lds + i * kChunk * VS, x4, cm);
+                stage_rows<VS, 1, true>(E, V, i * kChunk, min(kChunk, T - i * kChunk), lds + i * kBufFloats, x4, cm);
             wait_vm();
         }
         // chunk 0's column 0: from the staged rows, or (a column-only helper, which cannot
@@ -733,7 +950,7 @@ struct Forward {
             if (stage) {
                 column0(0, T, inf_from, lds, c0b, acc);
             } else {  // chunk 0 column 0 into the 4th buffer (first staged after barrier 0)
-                float* own = lds + 3 * kChunk * VS;
+                float* own = lds + 3 * kBufFloats;
                 if (lane_id() < min(kChunk, T)) own[lane_id() * VS] = E[(int64_t)lane_id() * V];
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 column0(0, T, inf_from, own, c0b, acc);
@@ -759,10 +976,10 @@ struct Forward {
             WX_T(h2);
             if (stage && q + 3 < nch)
                 stage_rows<VS, 1, true>(E, V, (q + 3) * kChunk, min(kChunk, T - (q + 3) * kChunk),
-                                        lds + ((q + 3) % kBufs) * kChunk * VS, x4, cm);
+                                        lds + ((q + 3) % kBufs) * kBufFloats, x4, cm);
             WX_T(h3);
             if (col0 && q + 1 < nch)
-                column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kChunk * VS, c0b, acc);
+                column0(q + 1, T, inf_from, lds + ((q + 1) % kBufs) * kBufFloats, c0b, acc);
             WX_T(h4);
 #ifdef WX_PHASE_TIMING
             acc_c0 += h4 - h3;
@@ -2454,6 +2671,16 @@ int launch_status() {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Development builds for A/B timing of V <= 32 batches (tools/ab): -DWX_DEV_V32 instantiates
+// the V <= 32 kernels only (a third of the compile time); wider vocabularies are NOT served.
+#ifdef WX_DEV_V32
+#define WX_VS64 32
+#define WX_VSG 32
+#else
+#define WX_VS64 64
+#define WX_VSG kGatherVS
+#endif
+
 // Kernels of different (C, W) buckets are independent: a batch that spans several buckets
 // forks them onto a small per-device pool of non-blocking streams and joins back onto the
 // caller's stream with events, so they run concurrently (a latency-bound batch then costs
@@ -2739,16 +2966,16 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
         if (ids[i] == (bucket_make(CC, WW, 1) | kSplitFlag)) {                                          \
             const dim3 g2(split_grid(S, a.parts)), b2(kWave * (WW + 2));                                 \
             if (V <= 32) hipLaunchKernelGGL((align_dp_split_kernel<CC, 32, WW>), g2, b2, 0, s, a);       \
-            else if (V <= 64) hipLaunchKernelGGL((align_dp_split_kernel<CC, 64, WW>), g2, b2, 0, s, a);  \
-            else hipLaunchKernelGGL((align_dp_split_kernel<CC, kGatherVS, WW>), g2, b2, 0, s, a);        \
+            else if (V <= 64) hipLaunchKernelGGL((align_dp_split_kernel<CC, WX_VS64, WW>), g2, b2, 0, s, a);  \
+            else hipLaunchKernelGGL((align_dp_split_kernel<CC, WX_VSG, WW>), g2, b2, 0, s, a);        \
         }
         WX_SPLIT_BUCKETS(WX_LAUNCH_SPLIT)
 #undef WX_LAUNCH_SPLIT
 #define WX_LAUNCH_ALIGN(CC, WW, HH)                                                                  \
         if (ids[i] == bucket_make(CC, WW, HH)) {                                                       \
             if (V <= 32) launch_align_dp<CC, 32, WW, HH>(grid, s, a);                                  \
-            else if (V <= 64) launch_align_dp<CC, 64, WW, HH>(grid, s, a);                             \
-            else launch_align_dp<CC, kGatherVS, WW, HH>(grid, s, a);                                   \
+            else if (V <= 64) launch_align_dp<CC, WX_VS64, WW, HH>(grid, s, a);                             \
+            else launch_align_dp<CC, WX_VSG, WW, HH>(grid, s, a);                                   \
         }
         WX_BUCKETS(WX_LAUNCH_ALIGN)
 #undef WX_LAUNCH_ALIGN
@@ -2801,8 +3028,8 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
 #define WX_LAUNCH_TR(CC, WW, HH)                                                                        \
         if (!HH && ids[i] == bucket_make(CC, WW, 0)) {                                                \
             if (V <= 32) hipLaunchKernelGGL((trellis_kernel<CC, 32, WW>), grid, dim3(kWave * WW), 0, s, a); \
-            else if (V <= 64) hipLaunchKernelGGL((trellis_kernel<CC, 64, WW>), grid, dim3(kWave * WW), 0, s, a); \
-            else hipLaunchKernelGGL((trellis_kernel<CC, kGatherVS, WW>), grid, dim3(kWave * WW), 0, s, a); \
+            else if (V <= 64) hipLaunchKernelGGL((trellis_kernel<CC, WX_VS64, WW>), grid, dim3(kWave * WW), 0, s, a); \
+            else hipLaunchKernelGGL((trellis_kernel<CC, WX_VSG, WW>), grid, dim3(kWave * WW), 0, s, a); \
         }
         WX_BUCKETS(WX_LAUNCH_TR)
 #undef WX_LAUNCH_TR

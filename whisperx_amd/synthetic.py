@@ -34,6 +34,20 @@ def w2v_dictionary():
     return {c.lower(): i for i, c in enumerate(W2V_VOCAB)}
 
 
+# A German character vocabulary of BASELINE config 5's size (V = 40), laid out like the HF
+# xlsr CTC tokenizers the DEFAULT_ALIGN_MODELS_HF entries use: '<pad>' first (the blank),
+# '|' for the word boundary, lower-case letters with umlauts and sharp s.
+DE_VOCAB = ["<pad>", "<s>", "</s>", "<unk>", "|", "'", "-"] + list("abcdefghijklmnopqrstuvwxyz") + \
+           ["ä", "ö", "ü", "ß", "é", "à", "."]
+DE_LETTERS = "enisratdhulcgmobwfkzvpüäößjyxq"
+
+
+def de_dictionary():
+    """config 5's {char: id} (V = 40, '<pad>' = 0 the blank)."""
+    assert len(DE_VOCAB) == 40
+    return {c: i for i, c in enumerate(DE_VOCAB)}
+
+
 def corpus_durations(seed: int = 4, n_files: int = 40, total_s: float = 36000.0, lo_s: float = 60.0,
                      hi_s: float = 3600.0) -> List[float]:
     """Log-uniform durations in [lo_s, hi_s], rescaled to sum to total_s (clipped, re-spread)."""
@@ -64,11 +78,11 @@ class Transcriber:
     """ASR stand-in: each VAD chunk becomes a segment {start, end, text} with start/end
     rounded to 3 decimals (asr.py:226-232) and ~14 chars/s of random words."""
 
-    def __init__(self, seed: int, pool_words: int = 200_000):
+    def __init__(self, seed: int, pool_words: int = 200_000, letters: str = LETTERS):
         rng = np.random.default_rng(seed)
         lens = rng.integers(2, 9, pool_words)
-        letters = rng.integers(0, len(LETTERS), int(lens.sum()))
-        text = np.array(list(LETTERS))[letters]
+        idx = rng.integers(0, len(letters), int(lens.sum()))
+        text = np.array(list(letters))[idx]
         cuts = np.concatenate([[0], np.cumsum(lens)])
         self.words = ["".join(text[cuts[i]:cuts[i + 1]]) for i in range(pool_words)]
         self.pos = 0
