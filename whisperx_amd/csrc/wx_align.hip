@@ -213,36 +213,11 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, i
 // read then gives a lane 4 steps of its token's column (and, read at a uniform address, 4
 // steps of the blank), instead of one or two dwords per step.  Column VS of each quad is not
 // staged: the column-0 helper writes the column-1 wave's lane-0 operand there (see
-// Forward::col0_pre).  LDS-DMA writes lane-linear: one dword per lane, lane i carrying row
-// 4p + (i & 3), column 16h + (i >> 2) of half h, lands exactly at p * QS + 64 h + i.
+// Forward::col0_pre).  The stager fills it from a row-major LDS-DMA ring (Forward::transpose_quads).
 template <int VS>
 __host__ __device__ constexpr int quad_stride() { return 4 * (VS + 1); }
 template <int VS>
 __host__ __device__ constexpr int quad_buf_floats() { return 8 * quad_stride<VS>(); }
-
-template <int VS>
-__device__ __forceinline__ void stage_quads(const float* __restrict__ E, int V, int r0, int nrows, float* dst) {
-    const int l = lane_id();
-    const unsigned base = (unsigned)uniform((int)lds_addr(dst));
-    const int r = l & 3;
-#pragma unroll
-    for (int p = 0; p < kChunk / 4; ++p) {
-        if (4 * p >= nrows) break;  // (uniform)
-#pragma unroll
-        for (int h = 0; h < VS / 16; ++h) {
-            const int c = 16 * h + (l >> 2);
-            if (c < V && 4 * p + r < nrows)
-                glds_dword(E + (int64_t)(r0 + 4 * p) * V, (unsigned)(r * V + c) * 4u,
-                           base + (unsigned)((p * quad_stride<VS>() + 64 * h) * 4));
-        }
-    }
-}
-// LDS-DMA instructions stage_quads issues for a chunk of `nrows` rows (the helper's vmcnt: a
-// half whose every lane is masked, 16 h >= V, is branched over and never issued)
-template <int VS>
-__device__ __forceinline__ int quad_loads(int nrows, int V) {
-    return nrows <= 0 ? 0 : ((nrows + 3) / 4) * min(VS / 16, (V + 15) / 16);
-}
 
 // The column map of one segment (all threads of the workgroup): columns 0 and `blank` and
 // every token id (ids outside [0, V) count as 0, as the DP reads them).  Returns the compact
@@ -296,19 +271,6 @@ __device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, i
 }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// s_waitcnt vmcnt with a (uniform) runtime count: waits until at most the largest of a few
-// immediates <= n of this wave's vector-memory operations are outstanding (over-waiting is
-// always correct: a smaller count only waits for more).
-__device__ __forceinline__ void wait_vm_le(int n) {
-    if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 __device__ __forceinline__ void wave_fence() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -472,7 +434,11 @@ template <int C, int VS, int MODE, int W, bool H, bool SP = false, int NH = 1>
 struct Forward {
     static constexpr int kRowBytes = VS * 4;
     static constexpr int kLanes = kWave * W;  // bitmap word stride (DP waves; SP: Split::lanes)
-    static constexpr int kBufs = H ? 4 : 2;   // emission chunk buffers in LDS
+    // emission chunk buffers in LDS; kReg (declared below) keeps five: its helper restages
+    // chunk q + 4 at barrier q into the buffer of chunk q - 1, the newest one no wave may still
+    // be reading (the DP waves read chunk q's operands until chunk q's first step, after
+    // barrier q — chunk 0's only after barrier 0)
+    static constexpr int kBufs = (C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS) ? 5 : (H ? 4 : 2);
     // Software-pipelined LDS operands where the extra registers keep the occupancy that
     // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
@@ -559,7 +525,7 @@ struct Forward {
             if constexpr (kReg) {
                 int t0 = N > 0 ? tok[d.tok0] : 0;
                 t0 = (t0 >= 0 && t0 < V) ? t0 : 0;
-                helper_reg(d, E, V, lds, nch, t0, col0, wv == W);
+                helper_reg(d, E, V, lds, lds + kBufs * kBufFloats, nch, t0, col0, wv == W, x4);
             } else {
                 helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
             }
@@ -827,17 +793,24 @@ struct Forward {
     "v_cmp_gt_f32 vcc, %[c], %[s]\n\t"                                                              \
     "v_maximum3_f32 %[" #NC "], %[s], %[c], %[c]\n\t"                                               \
     "v_addc_co_u32 %[w], vcc, %[w], %[w], vcc\n\t"
+#define WX_REG_OPERANDS                                                                                 \
+    : [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3]), [w] "+v"(w), [s] "=&v"(s),  \
+      [c] "=&v"(c)                                                                                          \
+    : [cur] "v"(cur), [e0] "v"(et.x), [e1] "v"(et.y), [e2] "v"(et.z), [e3] "v"(et.w), [b0] "v"(eb.x),     \
+      [b1] "v"(eb.y), [b2] "v"(eb.z), [b3] "v"(eb.w)                                                         \
+    : "vcc"
+    template <bool FIRST>  // FIRST: `cur` may have just been written by a VALU op (halo copy-in)
     __device__ __forceinline__ static void reg_steps4(float cur, unsigned& w, const float4& et, const float4& eb,
                                                       float (&n)[4]) {
         float s, c;
-        asm volatile(WX_REG_STEP(cur, n0, e0, b0) WX_REG_STEP(n0, n1, e1, b1) WX_REG_STEP(n1, n2, e2, b2)
-                         WX_REG_STEP(n2, n3, e3, b3)
-                     : [n0] "=&v"(n[0]), [n1] "=&v"(n[1]), [n2] "=&v"(n[2]), [n3] "=&v"(n[3]), [w] "+v"(w),
-                       [s] "=&v"(s), [c] "=&v"(c)
-                     : [cur] "v"(cur), [e0] "v"(et.x), [e1] "v"(et.y), [e2] "v"(et.z), [e3] "v"(et.w),
-                       [b0] "v"(eb.x), [b1] "v"(eb.y), [b2] "v"(eb.z), [b3] "v"(eb.w)
-                     : "vcc");
+        if constexpr (FIRST)
+            asm volatile("s_nop 1\n\t" WX_REG_STEP(cur, n0, e0, b0) WX_REG_STEP(n0, n1, e1, b1)
+                             WX_REG_STEP(n1, n2, e2, b2) WX_REG_STEP(n2, n3, e3, b3) WX_REG_OPERANDS);
+        else
+            asm volatile(WX_REG_STEP(cur, n0, e0, b0) WX_REG_STEP(n0, n1, e1, b1) WX_REG_STEP(n1, n2, e2, b2)
+                             WX_REG_STEP(n2, n3, e3, b3) WX_REG_OPERANDS);
     }
+#undef WX_REG_OPERANDS
 #undef WX_REG_STEP
     // 32 steps on operands `o`, issuing the next chunk's operand reads (n, from buffer nb) one
     // quad ahead of each group of four steps; column N history stored by the owner lane (rows
@@ -846,15 +819,16 @@ struct Forward {
                                                      float& cur, unsigned& w, bool owner, float* __restrict__ cn,
                                                      int t0, int T) {
         float hist[8];
-        // the first DPP may read a value a VALU op just wrote (halo copy-in): two wait states
-        asm volatile("s_nop 1");
 #pragma unroll
         for (int p = 0; p < kChunk / 4; ++p) {
             n.et[p] = *reinterpret_cast<const float4*>(nb + p * kQS * 4 + etq);
             n.eb[p] = *reinterpret_cast<const float4*>(nb + p * kQS * 4 + ebq);
             __builtin_amdgcn_sched_barrier(0);
             float nv[4];
-            reg_steps4(cur, w, o.et[p], o.eb[p], nv);
+            if (p == 0)
+                reg_steps4<true>(cur, w, o.et[p], o.eb[p], nv);
+            else
+                reg_steps4<false>(cur, w, o.et[p], o.eb[p], nv);
 #pragma unroll
             for (int j = 0; j < 4; ++j) hist[(4 * p + j) & 7] = nv[j];
             cur = nv[3];
@@ -875,56 +849,138 @@ struct Forward {
     }
     // tr[t][0] + em[t, tok[0]] for the rows of chunk q (the column-1 wave's lane-0 operand),
     // into column VS of the chunk's quad buffer.  tr[t][0] (alignment.py:367-370): 0 at t = 0,
-    // fp32 of the fp64 sum of em[0..t-1, 0] (torch CPU cumsum accumulates in double), +inf in
-    // the last N rows.  The fp64 chain runs on wave-uniform values (16-byte broadcast reads).
+    // fp32 of the fp64 sum of em[0..t-1, 0] (torch CPU cumsum accumulates in double, in row
+    // order), +inf in the last N rows.
+    // The prefix sums are formed lane-parallel without reassociating: lane 32 + i starts with
+    // em[t0 + i, 0], lanes 0..31 with +0, and at step j every lane adds its value and then takes
+    // its right neighbour's (DPP wave_shl:1, zero-filled).  Lane r (0..32) so adds exactly
+    // em[t0 + 0 .. r - 1, 0], in row order, into the running sum S(t0): it ends holding S(t0 + r)
+    // — the same fp64 additions, in the same order, as the sequential chain — and adding +0 is
+    // exact (the sum is never -0).  Three VALU per row, no exec juggling (a uniform chain with
+    // per-row conversions and broadcasts measured ~38 cycles per row, slower than the DP
+    // chunk it feeds).
     __device__ __forceinline__ static void col0_pre(int q, const SegDesc& d, float* buf, int tok0, double& acc) {
         const int T = d.T, N = d.N;
-        float4 e0[kChunk / 4], et[kChunk / 4];
+        const int l = lane_id();
+        const int rr = l & 31;
+        const float e = buf[(rr >> 2) * kQS + (rr & 3)];  // column 0 of row rr
+        float x = l >= 32 ? e : 0.0f;
+        double a = acc;
 #pragma unroll
-        for (int p = 0; p < kChunk / 4; ++p) {
-            e0[p] = *reinterpret_cast<const float4*>(buf + p * kQS);
-            et[p] = *reinterpret_cast<const float4*>(buf + p * kQS + 4 * tok0);
+        for (int j = 0; j < kChunk; ++j) {
+            a += (double)x;
+            x = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x130 /* wave_shl:1 */,
+                                                                   0xF, 0xF, true));
+        }
+        acc = __shfl(a, 32);  // S(t0 + 32): the next chunk's start (uniform)
+        if (l < 32) {
+            const int t = q * kChunk + l;
+            const float v = col0_value(t, a, T, N) + buf[(l >> 2) * kQS + 4 * tok0 + (l & 3)];
+            buf[(l >> 2) * kQS + 4 * VS + (l & 3)] = v;
+        }
+    }
+    // Staging of the quad layout.  Rows are first copied row-major into a ring of kRing raw
+    // chunk buffers by 16-byte LDS-DMA (stage_rows: 4 instructions per chunk when V == 32,
+    // issued kRing - 1 chunks ahead, so each chunk has two chunk-times to land), then
+    // transposed LDS -> LDS into the quad buffer: lane i reads the 4 rows of its (row quad,
+    // column) pairs (two ds_read2_b32) and writes them as one 16-byte store.  (One-dword LDS-DMA
+    // straight into the quad layout needs 16 instructions per chunk: measured ~1,600 cycles of
+    // issue per chunk, more than a DP chunk; register staging one chunk ahead stalled on the
+    // loads.)
+    static constexpr int kRing = 4;
+    static constexpr int kPairs = 8 * VS / kWave;  // (row quad, column) pairs per lane
+    __device__ __forceinline__ static void transpose_quads(const float* raw, float* buf) {
+        const int l = lane_id();
+        float v[kPairs][4];
+#pragma unroll
+        for (int m = 0; m < kPairs; ++m) {
+            const int k = kWave * m + l, p = k / VS, col = k % VS;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[m][j] = raw[(4 * p + j) * VS + col];
         }
 #pragma unroll
-        for (int p = 0; p < kChunk / 4; ++p) {
-            float v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int t = q * kChunk + 4 * p + j;
-                v[j] = col0_value(t, acc, T, N) + comp(et[p], j);
-                acc += (double)comp(e0[p], j);
-            }
-            if (lane_id() == 0) *reinterpret_cast<float4*>(buf + p * kQS + 4 * VS) = make_float4(v[0], v[1], v[2], v[3]);
+        for (int m = 0; m < kPairs; ++m) {
+            const int k = kWave * m + l, p = k / VS, col = k % VS;
+            *reinterpret_cast<float4*>(buf + p * kQS + 4 * col) = make_float4(v[m][0], v[m][1], v[m][2], v[m][3]);
         }
     }
     // The two helpers of a register-resident split kernel.  Barriers: -1, then one per chunk.
-    // Wave W stages quads four chunks ahead and makes chunks <= q + 2 land before barrier q;
-    // wave W + 1 (part 0 only) writes col0_pre of chunks 0 and 1 after barrier -1 and of chunk
-    // q + 2 after barrier q.  So after barrier q the DP waves can read chunk q + 1's operands,
-    // col0_pre included, while they compute chunk q; buffer q % 4 is restaged with chunk q + 4
-    // after barrier q (its rows were read during chunk q - 1, its col0_pre during chunk q - 2).
-    __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, int nch,
-                                      int tok0, bool col0, bool stage) {
+    // Wave W (the stager) makes chunk q + 2's quad buffer ready before barrier q (transposed
+    // out of the raw ring, its DMA issued two iterations earlier); wave W + 1 (part 0 only)
+    // writes col0_pre of chunks 0 and 1 after barrier -1 and of chunk q + 2 after barrier q.
+    // So after barrier q the DP waves can read chunk q + 1's operands, col0_pre included,
+    // while they compute chunk q.  Quad buffer (q + 2) % kBufs (five) last held chunk q - 3,
+    // whose operand reads the DP waves waited for before chunk q - 3's steps and whose column
+    // 0 the helper read during chunk q - 5.
+    __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* raw,
+                                      int nch, int tok0, bool col0, bool stage, bool x4) {
         const int T = d.T;
         auto buf = [&](int q) { return lds + (q % kBufs) * kBufFloats; };
+        auto ring = [&](int q) { return raw + (q % kRing) * kChunk * VS; };
         auto rows_of = [&](int q) { return (q >= 0 && q < nch) ? min(kChunk, T - q * kChunk) : 0; };
-        auto loads = [&](int q) { return quad_loads<VS>(rows_of(q), V); };
+        const ColMap cm{};  // (VS != kGatherVS: unused)
+        auto issue = [&](int q) {
+            if (q < nch) stage_rows<VS, 1, true>(E, V, q * kChunk, rows_of(q), ring(q), x4, cm);
+        };
+        // waits by DMA instruction count (stage_rows: one 16-byte instruction per 8 rows, else one
+        // per row)
+        auto wait_all_but = [&](int q) {  // all but chunk q's DMA instructions landed
+            const int n = q < nch ? (x4 && VS == 32 ? (rows_of(q) + 7) / 8 : rows_of(q)) : 0;
+            if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
         if (stage) {
-            for (int i = 0; i < 4 && i < nch; ++i) stage_quads<VS>(E, V, i * kChunk, rows_of(i), buf(i));
-            wait_vm_le(loads(2) + loads(3));  // barrier -1 needs chunks 0 and 1
+            for (int q = 0; q < kRing - 1; ++q) issue(q);
+            wait_vm();
+            transpose_quads(ring(0), buf(0));
+            if (nch > 1) transpose_quads(ring(1), buf(1));
+            issue(kRing - 1);
         }
         double acc = 0.0;
+#ifdef WX_HELPER_PRIO
+        if (col0) __builtin_amdgcn_s_setprio(WX_HELPER_PRIO);
+#endif
         __syncthreads();  // barrier -1
         if (col0) {
             col0_pre(0, d, buf(0), tok0, acc);
             if (nch > 1) col0_pre(1, d, buf(1), tok0, acc);
         }
+#ifdef WX_PHASE_TIMING
+        unsigned long long acc_work = 0, acc_bar = 0, acc_vm = 0;
+#endif
+        // one iteration: stage (chunk q + 2 transposed out of the ring — issued two iterations ago;
+        // chunk q + 3's DMA may still be in flight — then chunk q + kRing issued into the slot of
+        // chunk q, transposed two iterations ago), barrier q, column 0
         for (int q = 0; q < nch; ++q) {
-            if (stage) wait_vm_le(loads(q + 3));  // chunks <= q + 2 landed
-            __syncthreads();                      // barrier q
-            if (stage && q + 4 < nch) stage_quads<VS>(E, V, (q + 4) * kChunk, rows_of(q + 4), buf(q + 4));
+            WX_T(h0);
+            if (stage && q + 2 < nch) {
+                wait_all_but(q + 3);  // chunk q + 2's DMA landed (q + 3's may be in flight)
+                transpose_quads(ring(q + 2), buf(q + 2));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads done: the slot is free
+                issue(q + kRing);
+            }
+            WX_T(h1);
+            __syncthreads();  // barrier q
+            WX_T(h2);
             if (col0 && q + 2 < nch) col0_pre(q + 2, d, buf(q + 2), tok0, acc);
+            WX_T(h3);
+#ifdef WX_PHASE_TIMING
+            acc_vm += h1 - h0;
+            acc_bar += h2 - h1;
+            acc_work += h3 - h2;
+#endif
         }
+#ifdef WX_PHASE_TIMING
+        if (lane_id() == 0 && blockIdx.x < 8192) {  // [work, barrier wait, vmcnt wait] per helper
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W + (stage ? 0 : 1)) * 3;
+            o[0] = acc_work;
+            o[1] = acc_bar;
+            o[2] = acc_vm;
+        }
+#endif
     }
 
     // The helper wave (H): mirrors the DP waves' barriers.  Before barrier q, chunks q and
