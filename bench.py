@@ -247,6 +247,53 @@ def e2e_config3(device, seed=3):
                     "synthetic scores/audio/transcripts"}
 
 
+def _smooth_vad_scores(seed, F=213_333):
+    """Config 3's synthetic VAD scores: smoothed noise through a sigmoid (~2 regions/min)."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(F + 40)
+    y = np.convolve(x, np.ones(40) / 40, mode="valid")[:F] * 4 * np.sqrt(40) / 3
+    return (1 / (1 + np.exp(-y))).astype(np.float32)
+
+
+def binarize_1h(device, reps=20):
+    """Binarize on 1 h of scores (213,333 frames), the device-side call of merge_chunks:
+    smooth config-3 scores and dense ones (uniform noise thresholded at its median: an event
+    every ~2 frames, the random-weight producer's case), both kernels.  ms = HIP events
+    around _lib.binarize on device-resident scores (pre-pass + state machine + region
+    count read-back), best of reps; merge_chunks_dense_ms = the whole host call."""
+    from whisperx_amd import _lib
+    from whisperx_amd.vad import SlidingWindow, SlidingWindowFeature, merge_chunks
+
+    geom = [(0.0, 0.016875, 0.0619375)]
+    dense = np.random.default_rng(8).random(213_333).astype(np.float32)
+    med = float(np.median(dense))
+    cases = {"smooth": (_smooth_vad_scores(3), 0.5, 0.363), "dense": (dense, med, med)}
+    out = {}
+    for name, (y, on, off) in cases.items():
+        yd = torch.from_numpy(y).to(device)
+        for tp in (True, False):
+            ts = []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                (rs, _re), = _lib.binarize([yd], geom, on, off, 30.0, device=device, two_pass=tp)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            out[f"{name}_{'two' if tp else 'one'}_pass_ms"] = min(ts)
+        out[f"{name}_regions"] = int(len(rs))
+    feat = SlidingWindowFeature(torch.from_numpy(dense)[:, None].to(device), SlidingWindow(0.0, 0.016875, 0.0619375))
+    ws = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        chunks = merge_chunks(feat, 30, med, med)
+        ws.append(time.perf_counter() - t0)
+    out["merge_chunks_dense_ms"] = 1000 * min(ws)
+    out["merge_chunks_dense_chunks"] = len(chunks)
+    out["note"] = "1 h = 213,333 frames of 16.875 ms; max_duration 30 s"
+    return out
+
+
 def vad_producer_1h(device, seed=5, batch_size=2048):
     """VAD producer (vad.py:198-240) on 1 h of audio: 7,191 five-second windows every 0.5 s
     through the random-weight PyanNet-shaped segmentation model (batched) and the overlap-add
@@ -748,6 +795,10 @@ def main():
                 extra["e2e_align"] = e2e_align(device)
             except Exception as e:  # never let the secondary leg hide the primary line
                 extra["e2e_align"] = {"error": repr(e)[:200]}
+            try:
+                extra["binarize_1h"] = binarize_1h(device)
+            except Exception as e:
+                extra["binarize_1h"] = {"error": repr(e)[:300]}
             try:
                 extra["vad_producer_1h"] = vad_producer_1h(device)
             except Exception as e:

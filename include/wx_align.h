@@ -187,6 +187,17 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files,
                 double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
                 void* stream);
 
+/* wx_binarize in two passes with a caller-owned workspace (same results): a chip-wide pass
+ * writes per-64-frame onset/offset bit words and first-minimum records, then one wave per
+ * file jumps from event to event over them (cost per event, not per frame).  total_frames =
+ * f_off[n_files] (the host sizes the pre-pass grid from it). */
+size_t wx_binarize_workspace_bytes(int32_t n_files, int64_t total_frames);
+int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, int64_t total_frames,
+                   const double* sw_start, const double* sw_step, const double* sw_duration,
+                   float onset, float offset, double max_duration, double pad_onset, double pad_offset,
+                   double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
 /* Emission producer (alignment.py:226-233, the wav2vec2 forward): GroupNorm with one group
  * per channel (the first feature-encoder layer) over time-major activations x [L, C] (C % 4
  * == 0, 16-byte aligned), with the affine gamma/beta (may be NULL) and, when gelu != 0, the

@@ -69,6 +69,12 @@ def test_argument_validation_without_device(lib):
                                 dummy, dummy, 1 << 30, 7, None) == 1001  # unknown launch shape
     assert lib.wx_binarize(None, None, -1, None, None, None, 0.5, 0.3, 1.0, 0.0, 0.0, None, None, None, None,
                            None) == 1001
+    ws = lib.wx_binarize_workspace_bytes(3, 213334)
+    assert ws >= 24 * (213334 // 64 + 4)
+    assert lib.wx_binarize_ex(dummy, dummy, 3, 213334, dummy, dummy, dummy, 0.5, 0.3, 30.0, 0.0, 0.0, dummy, dummy,
+                              dummy, dummy, dummy, ws - 1, None) == 1004
+    assert lib.wx_binarize_ex(None, None, -1, 0, None, None, None, 0.5, 0.3, 1.0, 0.0, 0.0, None, None, None, None,
+                              None, 0, None) == 1001
 
 
 def test_launch_plan_bucket_selection(lib):

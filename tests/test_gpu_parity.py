@@ -581,3 +581,66 @@ def test_binarize_one_hour_vs_oracle():
     for i, (rs, re) in enumerate(outs):
         assert list(zip(rs.tolist(), re.tolist())) == oracle.binarize(cols[i], 0.25 * i, 0.016875, 0.0619375,
                                                                        0.5, 0.363, max_duration=30)
+
+
+def _binarize_both(cols, geom, onset, offset, maxd):
+    from whisperx_amd import _lib
+
+    two = _lib.binarize(cols, geom, onset, offset, maxd, two_pass=True)
+    one = _lib.binarize(cols, geom, onset, offset, maxd, two_pass=False)
+    for i, c in enumerate(cols):
+        want = oracle.binarize(c, *geom[i], onset, offset, max_duration=maxd)
+        for tag, (rs, re) in (("two-pass", two[i]), ("one-pass", one[i])):
+            assert list(zip(rs.tolist(), re.tolist())) == want, (tag, i, len(c), onset, offset, maxd)
+
+
+def test_binarize_dense_events_nan_and_ragged_files():
+    """The two-pass kernel (bit-word pre-pass + event-jumping state machine) and the one-pass
+    scan against the oracle where every other frame is an event (noise thresholded at its
+    median), min-cuts span many 64-frame blocks, blocks hold NaNs (np.argmin takes the first
+    NaN), and files are 0, 1, 63, 64, 65 ... frames long (partial words, words of one frame)."""
+    rng = np.random.default_rng(11)
+    lens = [1, 2, 63, 64, 65, 127, 128, 129, 1000, 4095, 4096, 4097, 9000, 30001]
+    cols = []
+    for k, n in enumerate(lens):
+        y = rng.random(n).astype(np.float32)
+        if k % 3 == 0 and n > 10:
+            y[rng.integers(0, n, max(n // 200, 1))] = np.nan
+        if k % 4 == 1:  # ties: quantised scores
+            y = np.round(y * 8) / 8
+        cols.append(y)
+    geom = [(0.1 * i, 0.016875, 0.0619375) for i in range(len(cols))]
+    for onset, offset, maxd in ((0.5, 0.5, 30.0), (0.5, 0.363, 1.0), (0.2, 0.1, 0.5), (0.95, 0.9, 0.05),
+                                (0.5, 0.4, float("inf")), (0.0, 0.0, 2.0)):
+        _binarize_both(cols, geom, onset, offset, maxd)
+
+
+def test_binarize_all_active_many_splits():
+    """Scores above onset everywhere: one region cut at every max_duration, each cut an argmin
+    over ~half the current list (block records + two partial blocks), with NaN runs and
+    constant stretches (ties go to the first frame)."""
+    rng = np.random.default_rng(12)
+    F = 50_000
+    y = (0.6 + 0.4 * rng.random(F)).astype(np.float32)
+    y[10_000:10_300] = 0.7  # a constant stretch: the first minimum wins
+    y[20_000:20_070] = np.nan
+    y[33_333] = np.nan
+    geom = [(0.0, 0.016875, 0.0619375)]
+    for maxd in (30.0, 7.3, 1.1, 0.02):
+        _binarize_both([y], geom, 0.5, 0.5, maxd)
+
+
+def test_binarize_and_merge_chunks_device_scores_dense():
+    """merge_chunks on device-resident dense-event scores equals the oracle's reference loop
+    over the oracle's regions (the VAD producer's untrained-model case)."""
+    import torch
+    from whisperx_amd.vad import SlidingWindow, SlidingWindowFeature, merge_chunks
+
+    rng = np.random.default_rng(13)
+    y = rng.random(213_333).astype(np.float32)
+    med = float(np.median(y))
+    sw = SlidingWindow(0.0, 0.016875, 0.0619375)
+    got = merge_chunks(SlidingWindowFeature(torch.from_numpy(y)[:, None].to("cuda:0"), sw), 30, onset=med, offset=med)
+    regs = oracle.binarize(y, 0.0, 0.016875, 0.0619375, med, med, max_duration=30)
+    want = oracle.merge_chunks_regions(regs, 30)
+    assert got == want

@@ -74,6 +74,9 @@ SIGNATURES = {
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
+    "wx_binarize_workspace_bytes": (_sz, [_i32, _i64]),
+    "wx_binarize_ex": (ctypes.c_int, [_vp, _vp, _i32, _i64, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
+                                      _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
 }
 
 
@@ -396,10 +399,11 @@ def merge_repeats(path_tok, path_time, path_prob, path_off, path_len, device):
 
 
 def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration: float,
-             pad_onset: float = 0.0, pad_offset: float = 0.0, device=None):
+             pad_onset: float = 0.0, pad_offset: float = 0.0, device=None, two_pass: bool = True):
     """Binarize score columns on the GPU.  scores_list: 1-D float32 arrays/tensors (one per
     column); sw_geometry: [(start, step, duration)] per column.  Returns [(starts, ends)]
-    as float64 numpy arrays per column."""
+    as float64 numpy arrays per column.  two_pass picks wx_binarize_ex (bit-word pre-pass +
+    event-jumping state machine; the default) or the one-pass scan wx_binarize."""
     import numpy as np
     lib = load()
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -424,10 +428,18 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
     cnt = torch.empty(max(len(F), 1), dtype=torch.int64, device=dev)
     f_off_d, r_off_d = _dev_i64(f_off, dev), _dev_i64(r_off, dev)  # referenced until enqueued
     with torch.cuda.device(dev):
-        _check(lib.wx_binarize(_ptr(ys), _ptr(f_off_d), len(F), _ptr(st0), _ptr(stp), _ptr(dur),
-                               float(np.float32(onset)), float(np.float32(offset)), float(max_duration),
-                               float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(r_off_d),
-                               _ptr(cnt), _stream(dev)))
+        if two_pass:
+            wsb = lib.wx_binarize_workspace_bytes(len(F), f_off[-1])
+            ws = _ws_emit.get(f"bin/{dev}/{torch.cuda.current_stream(dev).cuda_stream}", wsb, dev)
+            _check(lib.wx_binarize_ex(_ptr(ys), _ptr(f_off_d), len(F), f_off[-1], _ptr(st0), _ptr(stp), _ptr(dur),
+                                      float(np.float32(onset)), float(np.float32(offset)), float(max_duration),
+                                      float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(r_off_d),
+                                      _ptr(cnt), _ptr(ws), ws.numel(), _stream(dev)))
+        else:  # the one-pass event scan (wx_binarize)
+            _check(lib.wx_binarize(_ptr(ys), _ptr(f_off_d), len(F), _ptr(st0), _ptr(stp), _ptr(dur),
+                                   float(np.float32(onset)), float(np.float32(offset)), float(max_duration),
+                                   float(pad_onset), float(pad_offset), _ptr(rs), _ptr(re), _ptr(r_off_d),
+                                   _ptr(cnt), _stream(dev)))
     cnt_h = cnt.cpu().numpy()
     out = []
     for i in range(len(F)):

@@ -92,6 +92,20 @@ __device__ __forceinline__ float dpp_shr1(float old_lane0, float v) {
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(uint64_t)x);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ float uniformf(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+// lane l's 64-bit value, wave-uniform (two v_readlane)
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long x, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
 
 // Cell values live in an ext_vector so that the one dynamic (wave-uniform) index of the
 // step — the slot holding column N — lowers to s_set_gpr_idx_on/v_mov instead of scratch.
@@ -2519,6 +2533,42 @@ __device__ __forceinline__ void argmin_combine(float& v, int64_t& f, bool& nan, 
     }
 }
 
+// Region output of a Binarize wave: region n is held by lane n % 64 and the wave writes 64
+// at a time (one coalesced store per array).  A store per region made every later load of
+// the wave wait for the store's acknowledgement (vmcnt counts both, in order): ~0.5 us per
+// region on dense scores.
+struct RegionOut {
+    double* rs;
+    double* re;
+    int64_t cap;
+    int64_t n = 0;
+    bool overflow = false;
+    double bs = 0.0, be = 0.0;
+    __device__ __forceinline__ void emit(double s, double e, int lane) {
+        if (!((e - s) > 1e-6)) return;  // pyannote Segment truthiness: empty segments are not stored
+        if (n >= cap) {
+            overflow = true;
+            return;
+        }
+        if (lane == (int)(n & (kWave - 1))) {
+            bs = s;
+            be = e;
+        }
+        ++n;
+        if ((n & (kWave - 1)) == 0) {
+            rs[n - kWave + lane] = bs;
+            re[n - kWave + lane] = be;
+        }
+    }
+    __device__ __forceinline__ void flush(int lane) {
+        const int r = (int)(n & (kWave - 1));
+        if (lane < r) {
+            rs[n - r + lane] = bs;
+            re[n - r + lane] = be;
+        }
+    }
+};
+
 #ifndef WX_SCANQ
 #define WX_SCANQ 2
 #endif
@@ -2535,20 +2585,8 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
     const int64_t cap = a.reg_off[file + 1] - r0;
     double* rs = a.rs + r0;
     double* re = a.re + r0;
-    int64_t n = 0;
-    bool overflow = false;
-    auto emit = [&](double s, double e) {
-        if (!((e - s) > 1e-6)) return;  // pyannote Segment truthiness: empty segments are not stored
-        if (n >= cap) {
-            overflow = true;
-            return;
-        }
-        if (lane == 0) {
-            rs[n] = s;
-            re[n] = e;
-        }
-        ++n;
-    };
+    RegionOut out{rs, re, cap};
+    auto emit = [&](double s, double e) { out.emit(s, e, lane); };
     if (F <= 0) {
         if (lane == 0) a.reg_count[file] = 0;
         return;
@@ -2657,7 +2695,246 @@ __global__ __launch_bounds__(kWave) void binarize_kernel(BinarizeArgs a) {
         const double tl = (F == 1) ? sw_mid(st, step, dur, 0) : sw_mid(st, step, dur, F - 1);
         emit(start - a.pad_on, tl + a.pad_off);
     }
-    if (lane == 0) a.reg_count[file] = overflow ? -1 : n;
+    out.flush(lane);
+    if (lane == 0) a.reg_count[file] = out.overflow ? -1 : out.n;
+}
+
+// ------------------------------------------------------------------------------------
+// Binarize, two-pass form (wx_binarize_ex).  Pass 1 (binarize_words_kernel: one thread per
+// 64-frame block of every file, chip-wide) writes the block's onset word (bit k: y > onset),
+// offset word (bit k: y < offset) and first-minimum record (np.argmin order: the first NaN,
+// else the first smallest value).  Pass 2 (binarize_fsm_kernel: one wave per file) runs the
+// state machine event to event: the next activation / deactivation is the next set bit of
+// a word array, found in a window of 64 words (4096 frames) held one word per lane with the
+// following window prefetched; the first frame past max_duration comes from the window
+// geometry; a min-cut is the argmin over the records of the full blocks in its range and
+// the frames of the two partial blocks at its ends.  Cost per event is a few dozen wave
+// instructions, independent of the gap to the next event.  Block b of a file starting at
+// frame f0 is word (f0 >> 6) + file + b.
+struct BinWords {
+    unsigned long long* on;   // y > onset
+    unsigned long long* off;  // y < offset
+    float* mv;                // block minimum (NaN when the block holds one: the first)
+    int32_t* mi;              // its file-local frame; -1 for words past the file's end
+};
+
+__host__ __device__ inline int64_t bin_word_base(int64_t f0, int file) { return (f0 >> 6) + file; }
+inline int64_t bin_words(int64_t total_frames, int n_files) { return (total_frames >> 6) + n_files + 1; }
+
+struct BinWordArgs {
+    const float* y;
+    const int64_t* f_off;
+    int n_files;
+    int64_t n_words;
+    float onset, offset;
+    BinWords w;
+};
+
+__global__ __launch_bounds__(256) void binarize_words_kernel(BinWordArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.n_words) return;
+    int lo = 0, hi = a.n_files - 1;  // the last file whose first word is <= g
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (bin_word_base(a.f_off[mid], mid) <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t f0 = a.f_off[lo];
+    const int64_t F = a.f_off[lo + 1] - f0;
+    const int64_t fb = (g - bin_word_base(f0, lo)) << 6;
+    unsigned long long on = 0, off = 0;
+    float mv = 0.f;
+    int32_t mi = -1;
+    if (fb >= 0 && fb < F) {
+        const int n = (int)min<int64_t>(kWave, F - fb);
+        const float* y = a.y + f0 + fb;
+        bool nan = false;
+        // a uniform trip count with a per-lane predicate and selects: a loop whose exit is
+        // divergent let the compiler keep the (uniform) index of the last update in an SGPR
+        for (int k = 0; k < kWave; ++k) {
+            const bool in = k < n;
+            const float v = in ? y[k] : 0.f;
+            on |= (unsigned long long)(in && v > a.onset) << k;
+            off |= (unsigned long long)(in && v < a.offset) << k;
+            const bool vn = v != v;
+            const bool take = in && (mi < 0 || (!nan && (vn || v < mv)));
+            mv = take ? v : mv;
+            mi = take ? k : mi;
+            nan = take ? vn : nan;
+        }
+        mi += (int32_t)fb;
+    }
+    a.w.on[g] = on;
+    a.w.off[g] = off;
+    a.w.mv[g] = mv;
+    a.w.mi[g] = mi;
+}
+
+struct BinWin {  // words [base, base + 64) one per lane, and the next 64 prefetched
+    int64_t base;
+    unsigned long long w, nx;
+};
+
+__device__ __forceinline__ unsigned long long bin_ld(const unsigned long long* p, int64_t i, int64_t nw) {
+    return i < nw ? p[i] : 0ull;
+}
+
+// First frame >= from whose bit is set in p[0, nw), or -1.
+__device__ __forceinline__ int64_t bin_next(const unsigned long long* p, int64_t nw, BinWin& s, int64_t from,
+                                            int lane) {
+    int64_t wi = uniform64(from >> 6);
+    unsigned long long low = ~0ull << (from & 63);
+    while (wi < nw) {
+        s.base = uniform64(s.base);
+        if (wi >= s.base + kWave && wi < s.base + 2 * kWave) {
+            s.base += kWave;
+            s.w = s.nx;
+            s.nx = bin_ld(p, s.base + kWave + lane, nw);
+        } else if (wi < s.base || wi >= s.base + kWave) {
+            s.base = wi;
+            s.w = bin_ld(p, wi + lane, nw);
+            s.nx = bin_ld(p, wi + kWave + lane, nw);
+        }
+        const int k = (int)(wi - s.base);
+        unsigned long long x = s.w;
+        if (lane == k) x &= low;
+        const unsigned long long m = __ballot(lane >= k && x != 0ull);
+        if (m) {  // results made wave-uniform: the state machine around this runs as scalar code
+            const int l = __ffsll((long long)m) - 1;
+            const unsigned long long xw = readlane64(x, l);
+            return uniform64(((s.base + l) << 6) + (__ffsll((long long)xw) - 1));
+        }
+        wi = uniform64(s.base + kWave);
+        low = ~0ull;
+    }
+    return -1;
+}
+
+// np.argmin order over frames [fa, ev) (fa < ev) from the block records and the partial blocks.
+__device__ __forceinline__ void bin_argmin(const float* y, const float* mv, const int32_t* mi, int64_t fa,
+                                           int64_t ev, int lane, float& bv, int64_t& bf, bool& bn) {
+    bv = 0.f;
+    bf = -1;
+    bn = false;
+    const int64_t b0 = (fa + 63) >> 6, b1 = ev >> 6;
+    if (b0 >= b1) {  // no full block: at most 127 frames
+        for (int64_t f = fa + lane; f < ev; f += kWave) {
+            const float v = y[f];
+            argmin_combine(bv, bf, bn, v, f, v != v);
+        }
+    } else {
+        const int64_t fh = fa + lane, ft = (b1 << 6) + lane;
+        const float vh = fh < (b0 << 6) ? y[fh] : 0.f;
+        const float vt = ft < ev ? y[ft] : 0.f;
+        for (int64_t b = b0 + lane; b < b1; b += kWave) {
+            const float v = mv[b];
+            argmin_combine(bv, bf, bn, v, (int64_t)mi[b], v != v);
+        }
+        if (fh < (b0 << 6)) argmin_combine(bv, bf, bn, vh, fh, vh != vh);
+        if (ft < ev) argmin_combine(bv, bf, bn, vt, ft, vt != vt);
+    }
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const float v2 = __shfl_xor(bv, off);
+        const int64_t f2 = __shfl_xor(bf, off);
+        const bool n2 = __shfl_xor((int)bn, off) != 0;
+        argmin_combine(bv, bf, bn, v2, f2, n2);
+    }
+    bv = uniformf(bv);
+    bf = uniform64(bf);
+    bn = uniform((int)bn) != 0;
+}
+
+__global__ __launch_bounds__(kWave) void binarize_fsm_kernel(BinarizeArgs a, BinWords w) {
+    const int file = blockIdx.x;
+    const int lane = lane_id();
+    const int64_t f0 = a.f_off[file];
+    const int64_t F = a.f_off[file + 1] - f0;
+    const float* y = a.y + f0;
+    const double st = a.sw_start[file], step = a.sw_step[file], dur = a.sw_dur[file];
+    const int64_t r0 = a.reg_off[file];
+    const int64_t cap = a.reg_off[file + 1] - r0;
+    double* rs = a.rs + r0;
+    double* re = a.re + r0;
+    const int64_t wb = bin_word_base(f0, file), nw = (F + 63) >> 6;
+    const unsigned long long* won = w.on + wb;
+    const unsigned long long* woff = w.off + wb;
+    RegionOut out{rs, re, cap};
+    auto emit = [&](double s, double e) { out.emit(s, e, lane); };
+    if (F <= 0) {
+        if (lane == 0) a.reg_count[file] = 0;
+        return;
+    }
+    BinWin son{-(1ll << 40), 0ull, 0ull}, soff{-(1ll << 40), 0ull, 0ull};
+    double start = sw_mid(st, step, dur, 0);
+    // the split rule at frame f: mid(f) - start > max_duration; non-decreasing in f
+    auto past = [&](int64_t f) { return (sw_mid(st, step, dur, f) - start) > a.maxd; };
+    bool active = uniformf(y[0]) > a.onset;
+    bool has_stale = !active;  // curr = [0]: stale when inactive, else the range [0, 1)
+    int64_t stale = 0;
+    int64_t lo = active ? 0 : 1;
+    int64_t i = 1;
+    while (i < F) {
+        i = uniform64(i);
+        lo = uniform64(lo);
+        if (!active) {
+            const int64_t ev = bin_next(won, nw, son, i, lane);
+            if (ev < 0) break;
+            start = sw_mid(st, step, dur, ev);
+            active = true;
+            lo = ev + 1;  // the activation frame itself is not appended (vad.py:171-175)
+            i = ev + 1;
+            continue;
+        }
+        int64_t fd = bin_next(woff, nw, soff, i, lane);  // next deactivation frame
+        const int64_t last = fd < 0 ? F - 1 : fd;
+        if (!past(last)) {  // no split before the deactivation (the split rule is checked first)
+            if (fd < 0) break;
+            const double tev = sw_mid(st, step, dur, fd);
+            emit(start - a.pad_on, tev + a.pad_off);
+            start = tev;
+            active = false;
+            has_stale = true;
+            stale = fd;
+            i = fd + 1;
+            continue;
+        }
+        // first frame in [i, last] past max_duration: estimate from the geometry, then settle
+        const double x = (start + a.maxd - st - 0.5 * dur) / step;
+        int64_t ev = (x > (double)i) ? (x < (double)last ? (int64_t)x : last) : i;
+        while (ev > i && past(ev - 1)) --ev;
+        while (!past(ev)) ++ev;
+        // curr = [stale?] + frames [lo, ev); min-cut over positions [len/2, len)
+        const int64_t len = (has_stale ? 1 : 0) + (ev - lo);
+        const int64_t sa = len / 2;
+        const int64_t fa = lo + max<int64_t>(sa - (has_stale ? 1 : 0), 0);
+        float bv = 0.f;
+        int64_t bf = -1;
+        bool bn = false;
+        if (fa < ev) bin_argmin(y, w.mv + wb, w.mi + wb, fa, ev, lane, bv, bf, bn);
+        int64_t cut = bf;
+        bool cut_is_stale = false;
+        if (has_stale && sa == 0) {  // position 0 (the stale element) is a candidate and comes first
+            const float sv = uniformf(y[stale]);
+            const bool sn = sv != sv;
+            if (bf < 0 || sn || (!bn && !(bv < sv))) {
+                cut = stale;
+                cut_is_stale = true;
+            }
+        }
+        const double mt = sw_mid(st, step, dur, cut);
+        emit(start - a.pad_on, mt + a.pad_off);
+        start = mt;
+        if (!cut_is_stale) lo = cut + 1;
+        has_stale = false;
+        i = ev + 1;  // frame ev appended: range becomes [lo, ev+1)
+    }
+    if (active) {
+        const double tl = (F == 1) ? sw_mid(st, step, dur, 0) : sw_mid(st, step, dur, F - 1);
+        emit(start - a.pad_on, tl + a.pad_off);
+    }
+    out.flush(lane);
+    if (lane == 0) a.reg_count[file] = out.overflow ? -1 : out.n;
 }
 
 }  // namespace wx
@@ -3157,6 +3434,46 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, cons
     a.onset = onset; a.offset = offset; a.maxd = max_duration; a.pad_on = pad_onset; a.pad_off = pad_offset;
     a.rs = reg_start; a.re = reg_end; a.reg_off = reg_off; a.reg_count = reg_count;
     hipLaunchKernelGGL(binarize_kernel, dim3(n_files), dim3(kWave), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
+
+size_t wx_binarize_workspace_bytes(int32_t n_files, int64_t total_frames) {
+    if (n_files < 0 || total_frames < 0) return 0;
+    const size_t nw = (size_t)bin_words(total_frames, n_files);
+    return 2 * align_up(nw * 8u, 256) + 2 * align_up(nw * 4u, 256);
+}
+
+int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, int64_t total_frames,
+                   const double* sw_start, const double* sw_step, const double* sw_duration, float onset, float offset,
+                   double max_duration, double pad_onset, double pad_offset, double* reg_start, double* reg_end,
+                   const int64_t* reg_off, int64_t* reg_count, void* workspace, size_t workspace_bytes,
+                   void* stream) {
+    if (n_files < 0 || total_frames < 0) return WX_E_INVALID;
+    if (n_files == 0) return WX_OK;
+    if (!scores || !f_off || !sw_start || !sw_step || !sw_duration || !reg_start || !reg_end || !reg_off ||
+        !reg_count || !workspace)
+        return WX_E_INVALID;
+    if (workspace_bytes < wx_binarize_workspace_bytes(n_files, total_frames)) return WX_E_WORKSPACE;
+    const int64_t nw = bin_words(total_frames, n_files);
+    char* p = reinterpret_cast<char*>(workspace);
+    BinWords w;
+    w.on = reinterpret_cast<unsigned long long*>(p);
+    p += align_up((size_t)nw * 8u, 256);
+    w.off = reinterpret_cast<unsigned long long*>(p);
+    p += align_up((size_t)nw * 8u, 256);
+    w.mv = reinterpret_cast<float*>(p);
+    p += align_up((size_t)nw * 4u, 256);
+    w.mi = reinterpret_cast<int32_t*>(p);
+    BinWordArgs wa;
+    wa.y = scores; wa.f_off = f_off; wa.n_files = n_files; wa.n_words = nw; wa.onset = onset; wa.offset = offset;
+    wa.w = w;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(binarize_words_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, wa);
+    BinarizeArgs a;
+    a.y = scores; a.f_off = f_off; a.sw_start = sw_start; a.sw_step = sw_step; a.sw_dur = sw_duration;
+    a.onset = onset; a.offset = offset; a.maxd = max_duration; a.pad_on = pad_onset; a.pad_off = pad_offset;
+    a.rs = reg_start; a.re = reg_end; a.reg_off = reg_off; a.reg_count = reg_count;
+    hipLaunchKernelGGL(binarize_fsm_kernel, dim3(n_files), dim3(kWave), 0, s, a, w);
     return launch_status();
 }
 

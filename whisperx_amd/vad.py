@@ -193,12 +193,61 @@ def merge_chunks(segments, chunk_size, onset: float = 0.5, offset: Optional[floa
     regions into chunks no longer than chunk_size (unless a single region is)."""
     assert chunk_size > 0
     binarize = Binarize(max_duration=chunk_size, onset=onset, offset=offset)
-    ann = binarize(segments)
-    regions = [SegmentX(s.start, s.end, "UNKNOWN") for s in ann.get_timeline()]
-    if len(regions) == 0:
+    # no pads / min durations here, so the Annotation's timeline is the sorted set of the
+    # regions of all columns: taken from the region arrays without building the Annotation
+    s, e = _timeline(binarize.regions(segments))
+    if len(s) == 0:
         print("No active speech found in audio")
         return []
-    return _greedy_chunks(regions, chunk_size)
+    return _greedy_chunks_arrays(s, e, chunk_size)
+
+
+def _timeline(cols):
+    """Annotation.get_timeline() over the regions of every column: unique (start, end)
+    pairs in (start, end) order, as float64 arrays."""
+    if len(cols) == 1:
+        s, e = (np.asarray(x, dtype=np.float64) for x in cols[0])
+    else:
+        s = np.concatenate([np.asarray(c[0], dtype=np.float64) for c in cols]) if cols else np.zeros(0)
+        e = np.concatenate([np.asarray(c[1], dtype=np.float64) for c in cols]) if cols else np.zeros(0)
+    if len(s) > 1:
+        ordered = (s[1:] > s[:-1]) | ((s[1:] == s[:-1]) & (e[1:] > e[:-1]))
+        if not ordered.all():  # several columns (or out-of-order input): sort and drop repeats
+            o = np.lexsort((e, s))
+            s, e = s[o], e[o]
+            keep = np.ones(len(s), dtype=bool)
+            keep[1:] = (s[1:] != s[:-1]) | (e[1:] != e[:-1])
+            s, e = s[keep], e[keep]
+    return s, e
+
+
+def _greedy_chunks_arrays(s, e, chunk_size):
+    """_greedy_chunks over (start, end) arrays in timeline order.  With non-decreasing ends
+    (one VAD column always has them) the region that flushes a chunk started at cs is the
+    first later one with end - cs > chunk_size — a monotone predicate, so each chunk is one
+    binary search instead of a per-region loop; the regions are only touched to build the
+    chunks' segment lists."""
+    n = len(s)
+    if n > 1 and not bool(np.all(e[1:] >= e[:-1])):
+        return _greedy_chunks([SegmentX(a, b, "UNKNOWN") for a, b in zip(s.tolist(), e.tolist())], chunk_size)
+    sl, el = s.tolist(), e.tolist()
+    merged = []
+    if el[0] - sl[0] > chunk_size and 0 - sl[0] > 0:  # the reference's chunk_end = 0 start state
+        merged.append({"start": sl[0], "end": 0, "segments": []})
+    a = 0
+    while True:
+        cs = sl[a]
+        r = max(int(np.searchsorted(e, cs + chunk_size, side="right")), a + 1)
+        while r > a + 1 and el[r - 1] - cs > chunk_size:  # settle on the exact fp64 predicate
+            r -= 1
+        while r < n and not (el[r] - cs > chunk_size):
+            r += 1
+        # every region in (a, r) ends after cs (ends are non-decreasing and regions non-empty),
+        # so the reference's chunk_end - chunk_start > 0 condition holds at r
+        merged.append({"start": cs, "end": el[r - 1], "segments": list(zip(sl[a:r], el[a:r]))})
+        if r >= n:
+            return merged
+        a = r
 
 
 def _greedy_chunks(regions, chunk_size):
