@@ -598,9 +598,9 @@ def test_binarize_dense_events_nan_and_ragged_files():
     """The two-pass kernel (bit-word pre-pass + event-jumping state machine) and the one-pass
     scan against the oracle where every other frame is an event (noise thresholded at its
     median), min-cuts span many 64-frame blocks, blocks hold NaNs (np.argmin takes the first
-    NaN), and files are 0, 1, 63, 64, 65 ... frames long (partial words, words of one frame)."""
+    NaN), and files are 0, 1, 2, 63, 64, 65 ... frames long (partial words, words of one frame)."""
     rng = np.random.default_rng(11)
-    lens = [1, 2, 63, 64, 65, 127, 128, 129, 1000, 4095, 4096, 4097, 9000, 30001]
+    lens = [0, 1, 2, 63, 64, 65, 127, 128, 129, 1000, 4095, 4096, 4097, 0, 9000, 30001]
     cols = []
     for k, n in enumerate(lens):
         y = rng.random(n).astype(np.float32)

@@ -31,6 +31,8 @@ def words_np(y, onset, offset):
                 on[b] |= np.uint64(1) << np.uint64(k)
             if v < offset:
                 off[b] |= np.uint64(1) << np.uint64(k)
+        if b == 0 and not y[0] > onset:  # frame 0 decides the initial state: a reset when it does not activate
+            off[0] |= np.uint64(1)
         mi[b] = 64 * b + int(np.argmin(blk))
         mv[b] = blk[mi[b] - 64 * b]
     return on, off, mv, mi

@@ -2730,30 +2730,54 @@ struct BinWordArgs {
     BinWords w;
 };
 
-__global__ __launch_bounds__(256) void binarize_words_kernel(BinWordArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.n_words) return;
-    int lo = 0, hi = a.n_files - 1;  // the last file whose first word is <= g
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (bin_word_base(a.f_off[mid], mid) <= g) lo = mid;
-        else hi = mid - 1;
+// One wave per 64 words: the wave loads each word's 64 frames in one coalesced instruction
+// (lane = frame) into a padded LDS tile, then every lane scans its own word's column.  (A
+// lane reading its own 64 frames touched 64 cache lines per load instruction: 16 us per
+// hour against ~3 us.)
+__global__ __launch_bounds__(kWave) void binarize_words_kernel(BinWordArgs a) {
+    __shared__ float tile[kWave * (kWave + 1)];
+    const int lane = lane_id();
+    const int64_t g = (int64_t)blockIdx.x * kWave + lane;
+    int64_t gf = 0, fb = -1;  // this lane's word: first frame (global) and file-local
+    int n = 0;                // frames in it
+    if (g < a.n_words) {
+        int lo = 0, hi = a.n_files - 1;  // the last file whose first word is <= g
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (bin_word_base(a.f_off[mid], mid) <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t f0 = a.f_off[lo];
+        const int64_t F = a.f_off[lo + 1] - f0;
+        fb = (g - bin_word_base(f0, lo)) << 6;
+        if (fb < F) {
+            n = (int)min<int64_t>(kWave, F - fb);
+            gf = f0 + fb;
+        }
     }
-    const int64_t f0 = a.f_off[lo];
-    const int64_t F = a.f_off[lo + 1] - f0;
-    const int64_t fb = (g - bin_word_base(f0, lo)) << 6;
+    {
+        float v[kWave];  // all 64 loads in flight before the first wait
+#pragma unroll
+        for (int r = 0; r < kWave; ++r) {
+            const int64_t gr = (int64_t)readlane64((unsigned long long)gf, r);
+            const int nr = __builtin_amdgcn_readlane(n, r);
+            v[r] = a.y[gr + min(lane, max(nr - 1, 0))];
+        }
+#pragma unroll
+        for (int r = 0; r < kWave; ++r) tile[r * (kWave + 1) + lane] = v[r];
+    }
+    __syncthreads();
     unsigned long long on = 0, off = 0;
     float mv = 0.f;
     int32_t mi = -1;
-    if (fb >= 0 && fb < F) {
-        const int n = (int)min<int64_t>(kWave, F - fb);
-        const float* y = a.y + f0 + fb;
+    if (n > 0) {
         bool nan = false;
         // a uniform trip count with a per-lane predicate and selects: a loop whose exit is
         // divergent let the compiler keep the (uniform) index of the last update in an SGPR
+#pragma unroll 8
         for (int k = 0; k < kWave; ++k) {
+            const float v = tile[lane * (kWave + 1) + k];
             const bool in = k < n;
-            const float v = in ? y[k] : 0.f;
             on |= (unsigned long long)(in && v > a.onset) << k;
             off |= (unsigned long long)(in && v < a.offset) << k;
             const bool vn = v != v;
@@ -2763,11 +2787,16 @@ __global__ __launch_bounds__(256) void binarize_words_kernel(BinWordArgs a) {
             nan = take ? vn : nan;
         }
         mi += (int32_t)fb;
+        // frame 0 decides the initial state either way (vad.py:142): mark it a reset when it
+        // does not activate (the state machines never search the offset word at frame 0)
+        if (fb == 0 && !(on & 1ull)) off |= 1ull;
     }
-    a.w.on[g] = on;
-    a.w.off[g] = off;
-    a.w.mv[g] = mv;
-    a.w.mi[g] = mi;
+    if (g < a.n_words) {
+        a.w.on[g] = on;
+        a.w.off[g] = off;
+        a.w.mv[g] = mv;
+        a.w.mi[g] = mi;
+    }
 }
 
 struct BinWin {  // words [base, base + 64) one per lane, and the next 64 prefetched
@@ -2935,6 +2964,380 @@ __global__ __launch_bounds__(kWave) void binarize_fsm_kernel(BinarizeArgs a, Bin
     }
     out.flush(lane);
     if (lane == 0) a.reg_count[file] = out.overflow ? -1 : out.n;
+}
+
+// ------------------------------------------------------------------------------------
+// Binarize as a parallel scan (wx_binarize_ex when offset <= onset, the reference's
+// defaults and every whisperX call).  Without the max_duration rule the hysteresis state
+// after frame f is that of the last decisive frame <= f (y > onset: 1, y < offset: 0; no
+// frame is both when offset <= onset), so a 64-frame block's state word follows from its
+// onset / offset words and the state before it by one carry-propagate addition, and a
+// block's transfer function (state after it, per state before it) composes associatively.
+// binarize_scan_kernel (one 1024-thread workgroup per file) scans the blocks' transfer
+// functions, derives every block's activation (0 -> 1) and deactivation (1 -> 0) words and
+// scatters their frames, in order, into per-file region lists: region k runs from
+// activation a_k to deactivation d_k.  Wave 0 then takes the regions 64 at a time, one per
+// lane: a region that never exceeds max_duration (mid(d_k) - mid(a_k) <= max_duration; the
+// rule's predicate is non-decreasing in the frame) is emitted as it is.  The first one that
+// does runs the sequential active-state machine with min-cuts (bin_active_run) from a_k
+// until a deactivation that no split overrides: a split at a deactivation frame keeps the
+// region active (vad.py:150-161, `if ... elif`), so that machine may absorb the following
+// regions; the batch resumes at the first region activated after its end, where the real
+// and the scanned state agree again (a deactivation frame resets both).
+struct BinFile {
+    const float* y;
+    int64_t F;
+    double st, step, dur;
+    const unsigned long long* zw;  // offset words (frame 0's bit: a reset when it does not activate)
+    int64_t nw;
+    const float* mv;
+    const int32_t* mi;
+};
+
+// Active from frame i on (score list [stale?] + frames [lo, i), region start `start`) until
+// the first deactivation no split overrides (returned) or the file's end (-1, final region
+// emitted with the last frame's time, vad.py:178-180).
+__device__ int64_t bin_active_run(const BinarizeArgs& a, const BinFile& f, double start, bool has_stale,
+                                  int64_t stale, int64_t lo, int64_t i, RegionOut& out, int lane) {
+    BinWin soff{-(1ll << 40), 0ull, 0ull};
+    auto past = [&](int64_t fr) { return (sw_mid(f.st, f.step, f.dur, fr) - start) > a.maxd; };
+    while (true) {
+        i = uniform64(i);
+        lo = uniform64(lo);
+        if (i >= f.F) {
+            out.emit(start - a.pad_on, sw_mid(f.st, f.step, f.dur, f.F - 1) + a.pad_off, lane);
+            return -1;
+        }
+        const int64_t fd = bin_next(f.zw, f.nw, soff, i, lane);
+        const int64_t last = fd < 0 ? f.F - 1 : fd;
+        if (!past(last)) {
+            out.emit(start - a.pad_on, sw_mid(f.st, f.step, f.dur, last) + a.pad_off, lane);
+            return fd;
+        }
+        const double x = (start + a.maxd - f.st - 0.5 * f.dur) / f.step;
+        int64_t ev = (x > (double)i) ? (x < (double)last ? (int64_t)x : last) : i;
+        while (ev > i && past(ev - 1)) --ev;
+        while (!past(ev)) ++ev;
+        const int64_t len = (has_stale ? 1 : 0) + (ev - lo);
+        const int64_t sa = len / 2;
+        const int64_t fa = lo + max<int64_t>(sa - (has_stale ? 1 : 0), 0);
+        float bv = 0.f;
+        int64_t bf = -1;
+        bool bn = false;
+        if (fa < ev) bin_argmin(f.y, f.mv, f.mi, fa, ev, lane, bv, bf, bn);
+        int64_t cut = bf;
+        bool cut_is_stale = false;
+        if (has_stale && sa == 0) {
+            const float sv = uniformf(f.y[stale]);
+            const bool sn = sv != sv;
+            if (bf < 0 || sn || (!bn && !(bv < sv))) {
+                cut = stale;
+                cut_is_stale = true;
+            }
+        }
+        const double mt = sw_mid(f.st, f.step, f.dur, cut);
+        out.emit(start - a.pad_on, mt + a.pad_off, lane);
+        start = mt;
+        if (!cut_is_stale) lo = cut + 1;
+        has_stale = false;
+        i = ev + 1;
+    }
+}
+
+// State word of a block (bit k: state after frame k) from its onset word G, offset word Z
+// (disjoint) and the state before it: a carry generated at a G bit ripples up through the
+// keep bits and is absorbed at a Z bit.
+__device__ __forceinline__ unsigned long long bin_state_word(unsigned long long G, unsigned long long Z,
+                                                             unsigned s_in) {
+    const unsigned long long P = ~(G | Z);
+    const unsigned long long A = G | P;
+    return G | (P & ((A + G + (unsigned long long)s_in) ^ A ^ G));
+}
+
+// transfer functions as 2 bits (f(0) | f(1) << 1); "f then g"
+__device__ __forceinline__ unsigned tf_then(unsigned f, unsigned g) {
+    return ((g >> (f & 1u)) & 1u) | (((g >> ((f >> 1) & 1u)) & 1u) << 1);
+}
+
+constexpr int kBinWG = 1024;
+// Wave 0's regions are staged in an LDS ring and written out 2048 at a time: a store per
+// batch made the next batch's (prefetched) list loads wait for the stores too (vmcnt
+// counts both, in order).
+constexpr int kBinRing = 2048;
+constexpr int kBinChunk = 8;  // per-thread loads issued together in the scan kernel's passes
+
+// Exclusive scan over the workgroup in thread order ("a then b"), and the total.
+template <class T, class Op>
+__device__ __forceinline__ T wg_exclusive_scan(T x, T identity, Op op, T* lds, T& total) {
+    const int lane = lane_id(), wv = threadIdx.x / kWave;
+    T inc = x;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const T y = __shfl_up(inc, d);
+        if (lane >= d) inc = op(y, inc);
+    }
+    if (lane == kWave - 1) lds[wv] = inc;
+    __syncthreads();
+    T pre = identity, tot = identity;
+    for (int w = 0; w < kBinWG / kWave; ++w) {
+        const T v = lds[w];
+        if (w < wv) pre = op(pre, v);
+        tot = op(tot, v);
+    }
+    total = tot;
+    T ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = identity;
+    __syncthreads();
+    return op(pre, ex);
+}
+
+struct BinScanArgs {
+    BinarizeArgs a;
+    BinWords w;
+    int32_t* ra;  // activation frames, file at f_off[file] + file (capacity F + 1)
+    int32_t* rd;  // deactivation frames, same layout
+};
+
+__global__ __launch_bounds__(kBinWG) void binarize_scan_kernel(BinScanArgs sa) {
+    __shared__ unsigned s_f[kBinWG / kWave];
+    __shared__ unsigned long long s_n[kBinWG / kWave];
+    __shared__ double s_rs[kBinRing], s_re[kBinRing];
+    const BinarizeArgs& a = sa.a;
+    const int file = blockIdx.x;
+    const int t = threadIdx.x;
+    const int lane = lane_id();
+    const int64_t f0 = a.f_off[file];
+    const int64_t F = a.f_off[file + 1] - f0;
+    if (F <= 0) {
+        if (t == 0) a.reg_count[file] = 0;
+        return;
+    }
+    const int64_t nb = (F + 63) >> 6, wb = bin_word_base(f0, file);
+    const unsigned long long* G = sa.w.on + wb;
+    const unsigned long long* Z = sa.w.off + wb;
+    int32_t* ra = sa.ra + f0 + file;
+    int32_t* rd = sa.rd + f0 + file;
+    const int64_t per = (nb + kBinWG - 1) / kBinWG;
+    const int64_t b0 = min<int64_t>((int64_t)t * per, nb), b1 = min<int64_t>(b0 + per, nb);
+    // pass 1: this thread's blocks as a transfer function, and their transition counts for
+    // either state before them
+    unsigned s[2] = {0u, 1u};
+    unsigned long long cnt[2] = {0ull, 0ull};  // activations << 32 | deactivations
+    for (int64_t bc = b0; bc < b1; bc += kBinChunk) {  // loads of a chunk issued together
+        unsigned long long gv[kBinChunk], zv[kBinChunk];
+#pragma unroll
+        for (int j = 0; j < kBinChunk; ++j) {
+            const int64_t b = min<int64_t>(bc + j, b1 - 1);
+            gv[j] = G[b];
+            zv[j] = Z[b];
+        }
+#pragma unroll
+        for (int j = 0; j < kBinChunk; ++j) {
+            if (bc + j >= b1) break;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const unsigned long long S = bin_state_word(gv[j], zv[j], s[q]);
+                const unsigned long long prev = (S << 1) | s[q];
+                cnt[q] += ((unsigned long long)__popcll(S & ~prev) << 32) | (unsigned long long)__popcll(prev & ~S);
+                s[q] = (unsigned)(S >> 63);
+            }
+        }
+    }
+    unsigned ftot;
+    const unsigned fpre = wg_exclusive_scan(s[0] | (s[1] << 1), 2u, tf_then, s_f, ftot);
+    const unsigned s_in = fpre & 1u;  // inactive before frame 0
+    unsigned long long ntot;
+    const unsigned long long base =
+        wg_exclusive_scan(cnt[s_in], 0ull, [](unsigned long long x, unsigned long long y) { return x + y; }, s_n, ntot);
+    // pass 2: scatter the transition frames in order
+    int64_t ia = (int64_t)(base >> 32), id = (int64_t)(base & 0xffffffffull);
+    unsigned sv = s_in;
+    for (int64_t bc = b0; bc < b1; bc += kBinChunk) {
+        unsigned long long gv[kBinChunk], zv[kBinChunk];
+#pragma unroll
+        for (int j = 0; j < kBinChunk; ++j) {
+            const int64_t b = min<int64_t>(bc + j, b1 - 1);
+            gv[j] = G[b];
+            zv[j] = Z[b];
+        }
+        for (int j = 0; j < kBinChunk && bc + j < b1; ++j) {
+            const int64_t b = bc + j;
+            const unsigned long long S = bin_state_word(gv[j], zv[j], sv);
+            const unsigned long long prev = (S << 1) | sv;
+            unsigned long long act = S & ~prev, deact = prev & ~S;
+            while (act) {
+                ra[ia++] = (int32_t)((b << 6) + __ffsll((long long)act) - 1);
+                act &= act - 1;
+            }
+            while (deact) {
+                rd[id++] = (int32_t)((b << 6) + __ffsll((long long)deact) - 1);
+                deact &= deact - 1;
+            }
+            sv = (unsigned)(S >> 63);
+        }
+    }
+    __syncthreads();  // the lists are complete (workgroup-scope release/acquire)
+    const int64_t R = (int64_t)(ntot >> 32), ND = (int64_t)(ntot & 0xffffffffull);
+    const int64_t r0 = a.reg_off[file];
+    const int64_t cap = a.reg_off[file + 1] - r0;
+    double* rs = a.rs + r0;
+    double* re = a.re + r0;
+    BinFile f;
+    f.y = a.y + f0;
+    f.F = F;
+    f.st = a.sw_start[file];
+    f.step = a.sw_step[file];
+    f.dur = a.sw_dur[file];
+    // ---- no region exceeds max_duration (checked by all threads): every region is emitted as
+    // it is, at the position a workgroup prefix sum gives it
+    {
+        const int64_t perR = (R + kBinWG - 1) / kBinWG;
+        const int64_t k0 = min<int64_t>((int64_t)t * perR, R), k1 = min<int64_t>(k0 + perR, R);
+        auto region = [&](int64_t kk, int32_t av, int32_t dv, double& s, double& e) {  // 0 empty, 1 emitted, 2 long
+            const int64_t ak = av;
+            const int64_t ek = kk < ND ? (int64_t)dv : F - 1;
+            const double ts = sw_mid(f.st, f.step, f.dur, ak), te = sw_mid(f.st, f.step, f.dur, ek);
+            s = ts - a.pad_on;
+            e = te + a.pad_off;
+            return (te - ts) > a.maxd ? 2 : ((e - s) > 1e-6 ? 1 : 0);
+        };
+        // a chunk's list loads issued together
+        auto chunk = [&](int64_t kc, int32_t* av, int32_t* dv) {
+#pragma unroll
+            for (int j = 0; j < 2 * kBinChunk; ++j) {
+                const int64_t kk = min<int64_t>(kc + j, k1 - 1);
+                av[j] = ra[kk];
+                dv[j] = rd[min<int64_t>(kk, ND > 0 ? ND - 1 : 0)];
+            }
+        };
+        int64_t cnt_put = 0;
+        int any_long = 0;
+        for (int64_t kc = k0; kc < k1; kc += 2 * kBinChunk) {
+            int32_t av[2 * kBinChunk], dv[2 * kBinChunk];
+            chunk(kc, av, dv);
+#pragma unroll
+            for (int j = 0; j < 2 * kBinChunk; ++j) {
+                if (kc + j >= k1) break;
+                double s, e;
+                const int c = region(kc + j, av[j], dv[j], s, e);
+                any_long |= c == 2;
+                cnt_put += c == 1;
+            }
+        }
+        if (!__syncthreads_or(any_long)) {
+            unsigned long long tot;
+            const unsigned long long p0 = wg_exclusive_scan(
+                (unsigned long long)cnt_put, 0ull, [](unsigned long long x, unsigned long long y) { return x + y; },
+                s_n, tot);
+            int64_t p = (int64_t)p0;
+            for (int64_t kc = k0; kc < k1; kc += 2 * kBinChunk) {
+                int32_t av[2 * kBinChunk], dv[2 * kBinChunk];
+                chunk(kc, av, dv);
+#pragma unroll
+                for (int j = 0; j < 2 * kBinChunk; ++j) {
+                    if (kc + j >= k1) break;
+                    double s, e;
+                    if (region(kc + j, av[j], dv[j], s, e) == 1) {
+                        if (p < cap) {
+                            rs[p] = s;
+                            re[p] = e;
+                        }
+                        ++p;
+                    }
+                }
+            }
+            if (t == 0) a.reg_count[file] = (int64_t)tot > cap ? -1 : (int64_t)tot;
+            return;
+        }
+    }
+    if (t >= kWave) return;
+
+    // ---- wave 0: regions in order, 64 per batch
+    f.zw = Z;
+    f.nw = nb;
+    f.mv = sa.w.mv + wb;
+    f.mi = sa.w.mi + wb;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int64_t pos = 0, k = 0, last_deact = 0;  // frame 0 is the stale score before a first activation
+    bool overflow = false;
+    int64_t flushed = 0;  // regions [0, flushed) are out of the ring
+    auto flush_to = [&](int64_t upto) {
+        for (int64_t q = flushed + lane; q < upto && q < cap; q += kWave) {
+            rs[q] = s_rs[q & (kBinRing - 1)];
+            re[q] = s_re[q & (kBinRing - 1)];
+        }
+        flushed = upto;
+    };
+    // the next batch's lists are loaded one batch ahead (clamped, unconditional loads)
+    auto ld_a = [&](int64_t j) { return ra[min<int64_t>(j, R - 1)]; };
+    auto ld_d = [&](int64_t j) { return rd[min<int64_t>(j, ND > 0 ? ND - 1 : 0)]; };
+    int64_t pk = k;
+    int32_t pa = R > 0 ? ld_a(k + lane) : 0, pd = R > 0 ? ld_d(k + lane) : 0;
+    while (k < R) {
+        k = uniform64(k);
+        const int64_t kk = k + lane;
+        const bool valid = kk < R;
+        int32_t ca = pa, cd = pd;
+        if (pk != k) {
+            ca = ld_a(kk);
+            cd = ld_d(kk);
+        }
+        pk = k + kWave;
+        pa = ld_a(pk + lane);
+        pd = ld_d(pk + lane);
+        const int64_t ak = valid ? (int64_t)ca : 0;
+        const int64_t dk = (valid && kk < ND) ? (int64_t)cd : -1;
+        const int64_t ek = dk >= 0 ? dk : F - 1;
+        const double ts = sw_mid(f.st, f.step, f.dur, ak), te = sw_mid(f.st, f.step, f.dur, ek);
+        const unsigned long long lm = __ballot(valid && (te - ts) > a.maxd);
+        const int nn = lm ? __ffsll((long long)lm) - 1 : kWave;  // regions before the first long one
+        const double s = ts - a.pad_on, e = te + a.pad_off;
+        const bool put = valid && lane < nn && (e - s) > 1e-6;
+        const unsigned long long pm = __ballot(put);
+        if (pos + kWave - flushed > kBinRing) flush_to(pos);
+        const int64_t p = pos + __popcll(pm & lt);
+        if (put) {
+            s_rs[p & (kBinRing - 1)] = s;
+            s_re[p & (kBinRing - 1)] = e;
+        }
+        pos += __popcll(pm);
+        const int m = (int)min<int64_t>(nn, R - k);
+        if (m > 0) last_deact = uniform64(__shfl(dk, m - 1));
+        k += m;
+        if (!lm || k >= R) continue;
+        // region k exceeds max_duration: the sequential machine from its activation
+        const int64_t a0 = uniform64(__shfl(ak, nn));
+        flush_to(pos);
+        const int64_t room = pos < cap ? cap - pos : 0;
+        RegionOut out{rs + (cap - room), re + (cap - room), room};
+        const int64_t dstar = bin_active_run(a, f, sw_mid(f.st, f.step, f.dur, a0), a0 != 0, last_deact,
+                                             a0 == 0 ? 0 : a0 + 1, a0 + 1, out, lane);
+        out.flush(lane);
+        overflow |= out.overflow;
+        pos += out.n;
+        flushed = pos;
+        if (dstar < 0) break;
+        last_deact = dstar;
+        // resume at the first region activated after dstar
+        int64_t j0 = k + 1;
+        while (true) {
+            j0 = uniform64(j0);
+            const int64_t jj = j0 + lane;
+            const bool after = jj < R && (int64_t)ra[jj] > dstar;
+            const unsigned long long am = __ballot(after);
+            if (am) {
+                k = j0 + __ffsll((long long)am) - 1;
+                break;
+            }
+            j0 += kWave;
+            if (j0 >= R) {
+                k = R;
+                break;
+            }
+        }
+    }
+    flush_to(pos);
+    if (lane == 0) a.reg_count[file] = (overflow || pos > cap) ? -1 : pos;
 }
 
 }  // namespace wx
@@ -3440,7 +3843,8 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, cons
 size_t wx_binarize_workspace_bytes(int32_t n_files, int64_t total_frames) {
     if (n_files < 0 || total_frames < 0) return 0;
     const size_t nw = (size_t)bin_words(total_frames, n_files);
-    return 2 * align_up(nw * 8u, 256) + 2 * align_up(nw * 4u, 256);
+    const size_t nl = (size_t)total_frames + (size_t)n_files;  // region lists, F + 1 per file
+    return 2 * align_up(nw * 8u, 256) + 2 * align_up(nw * 4u, 256) + 2 * align_up(nl * 4u, 256);
 }
 
 int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, int64_t total_frames,
@@ -3464,16 +3868,28 @@ int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, i
     w.mv = reinterpret_cast<float*>(p);
     p += align_up((size_t)nw * 4u, 256);
     w.mi = reinterpret_cast<int32_t*>(p);
+    p += align_up((size_t)nw * 4u, 256);
+    const size_t nl = (size_t)total_frames + (size_t)n_files;
+    int32_t* ra = reinterpret_cast<int32_t*>(p);
+    p += align_up(nl * 4u, 256);
+    int32_t* rd = reinterpret_cast<int32_t*>(p);
     BinWordArgs wa;
     wa.y = scores; wa.f_off = f_off; wa.n_files = n_files; wa.n_words = nw; wa.onset = onset; wa.offset = offset;
     wa.w = w;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(binarize_words_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, wa);
+    if (total_frames > 0)  // (its tile loads read frame 0 for words past a file's end)
+        hipLaunchKernelGGL(binarize_words_kernel, dim3((unsigned)((nw + kWave - 1) / kWave)), dim3(kWave), 0, s, wa);
     BinarizeArgs a;
     a.y = scores; a.f_off = f_off; a.sw_start = sw_start; a.sw_step = sw_step; a.sw_dur = sw_duration;
     a.onset = onset; a.offset = offset; a.maxd = max_duration; a.pad_on = pad_onset; a.pad_off = pad_offset;
     a.rs = reg_start; a.re = reg_end; a.reg_off = reg_off; a.reg_count = reg_count;
-    hipLaunchKernelGGL(binarize_fsm_kernel, dim3(n_files), dim3(kWave), 0, s, a, w);
+    if (offset <= onset) {  // no frame both sets and resets: the parallel scan
+        BinScanArgs sa;
+        sa.a = a; sa.w = w; sa.ra = ra; sa.rd = rd;
+        hipLaunchKernelGGL(binarize_scan_kernel, dim3(n_files), dim3(kBinWG), 0, s, sa);
+    } else {
+        hipLaunchKernelGGL(binarize_fsm_kernel, dim3(n_files), dim3(kWave), 0, s, a, w);
+    }
     return launch_status();
 }
 
