@@ -1,11 +1,12 @@
 """One bench leg in isolation, for rocprofv3 runs (development tool): the program after
 `rocprofv3 ... --` runs exactly this leg's kernel K times after W warm-ups.
 
-    python tools/legs.py cfg2|sat3000|trellis3000 [--steps K] [--warmup W]
+    python tools/legs.py cfg2|sat3000|trellis3000|vad1h [--steps K] [--warmup W]
 
 cfg2: the headline step (64 x T=1499, V=32, wx_align_dp in the default shape);
 sat3000: 2048 x T=2999, V=32, N~U[850,951], wx_align_dp (throughput shape);
-trellis3000: get_trellis materialised (wx_trellis) on the sat3000 batch."""
+trellis3000: get_trellis materialised (wx_trellis) on the sat3000 batch;
+vad1h: the VAD producer (PyanNet-shaped segmentation forward + wx_vad_aggregate) over 1 h."""
 import argparse
 import os
 import sys
@@ -27,6 +28,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.leg == "vad1h":  # the VAD producer over 1 h of audio (warm-up: one whole hour)
+        from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+        torch.manual_seed(5)
+        vad = VoiceActivitySegmentation(device=dev, batch_size=2048)
+        wav = (torch.randn(1, 3600 * 16000, generator=torch.Generator().manual_seed(5)) * 0.1).to(dev)
+        vad({"waveform": wav, "sample_rate": 16000})
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.steps):
+            vad({"waveform": wav, "sample_rate": 16000})
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"vad1h: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, 1 h of audio", flush=True)
+        return
     if a.leg == "cfg2":
         ems, toks = make_batch(64, 1499, 32, 300, 500, 1000, dev)
     else:

@@ -102,6 +102,58 @@ class SincFilterbank(torch.nn.Module):
         return torch.cat(out, dim=0)
 
 
+_PATCH_BYTES = 1 << 30  # conv1d_batched: patch buffer per chunk of windows (Cin == 1)
+
+
+def conv1d_batched(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride: int) -> torch.Tensor:
+    """F.conv1d(x, w, b, stride) (no padding, dilation 1, one group) for a batch of windows
+    through a few large GEMMs.  MIOpen runs these shapes as one im2col + GEMM per window
+    (21,573 im2col launches per hour of audio: half the producer's GPU time,
+    profiles/r3_vad1h_kernel_stats.csv).  Returns [B, Cout, Lout] as the transposed view of a
+    time-major [B, Lout, Cout] buffer.
+
+    * Cin == 1 (the sinc filterbank, k = 251, stride 10): the taps are zero-padded to a multiple
+      of the stride, so patch row t is the contiguous slice x[s*t : s*t + k'] — an unfold view,
+      materialised for ~1 GB worth of windows at a time and multiplied by the [k', Cout] filters;
+    * Cin > 1, stride 1 (k = 5): the windows are flattened time-major into [B*L, Cin] and the
+      output is the sum over the k taps of one GEMM on the row-shifted view each; the rows that
+      straddle two windows (the last k - 1 of every window) are computed and dropped."""
+    B, Cin, L = x.shape
+    Cout, _, k = w.shape
+    Lout = (L - k) // stride + 1
+    if Cin == 1:
+        kp = -(-k // stride) * stride
+        xs = x.reshape(B, L)
+        if kp > k:
+            xs = F.pad(xs, (0, kp - k))
+        wp = F.pad(w.reshape(Cout, k), (0, kp - k)).t().contiguous()  # [kp, Cout]
+        pat = xs.unfold(1, kp, stride)[:, :Lout]  # [B, Lout, kp] view
+        out = torch.empty((B, Lout, Cout), dtype=x.dtype, device=x.device)
+        cb = max(1, _PATCH_BYTES // max(1, Lout * kp * x.element_size()))
+        for i in range(0, B, cb):
+            p = pat[i:i + cb].reshape(-1, kp)
+            o = out[i:i + cb].view(-1, Cout)
+            if b is not None:
+                torch.addmm(b, p, wp, out=o)
+            else:
+                torch.mm(p, wp, out=o)
+        return out.transpose(1, 2)
+    assert stride == 1
+    X = x.transpose(1, 2).reshape(B * L, Cin)  # time-major copy
+    R = B * L - k + 1
+    full = torch.empty((B * L, Cout), dtype=x.dtype, device=x.device)
+    wt = w.permute(2, 1, 0)  # [k, Cin, Cout]
+    for j in range(k):
+        if j == 0:
+            if b is not None:
+                torch.addmm(b, X[0:R], wt[0], out=full[:R])
+            else:
+                torch.mm(X[0:R], wt[0], out=full[:R])
+        else:
+            full[:R].addmm_(X[j:j + R], wt[j])
+    return full.view(B, L, Cout)[:, :Lout].transpose(1, 2)
+
+
 class SincEncoder(torch.nn.Module):
     """The filterbank as a bias-free strided convolution (asteroid Encoder).  The filters are
     a function of the band edges only: they are materialised once per parameter version and
