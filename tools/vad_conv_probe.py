@@ -1,6 +1,8 @@
 """VAD producer convolution probe (development tool): times SincNet's three convolutions at a
-2,048-window batch through MIOpen under several solver settings and through batched GEMM
-formulations, and the whole producer over 1 h.  Each MIOpen setting runs in its own process
+2,048-window batch through MIOpen under several solver settings, and the whole producer over
+1 h in steady state.  (Round 3, MI355X: sinc 15.5 ms, conv2 5.3 ms, conv3 1.8 ms per batch under
+every setting; batched-GEMM forms of the same convolutions measured 14.4 / 7.9 / 2.8 ms and were
+dropped; producer 199 ms per hour.)  Each MIOpen setting runs in its own process
 (MIOpen reads its environment once).
 
     python tools/vad_conv_probe.py"""
@@ -44,20 +46,9 @@ def child(tag):
         out["sinc_miopen_ms"] = timeit(lambda: F.conv1d(x0, w0, stride=10))
         out["conv2_miopen_ms"] = timeit(lambda: F.conv1d(x1, w1, b1))
         out["conv3_miopen_ms"] = timeit(lambda: F.conv1d(x2, w2, b2))
-        if tag == "gemm":
-            from whisperx_amd import vad_model
-
-            r0 = F.conv1d(x0[:64], w0, stride=10)
-            r1 = F.conv1d(x1[:64], w1, b1)
-            g0 = vad_model.conv1d_batched(x0[:64], w0, None, 10)
-            g1 = vad_model.conv1d_batched(x1[:64], w1, b1, 1)
-            out["sinc_gemm_maxrel"] = float(((g0 - r0).abs().max() / r0.abs().max()).item())
-            out["conv2_gemm_maxrel"] = float(((g1 - r1).abs().max() / r1.abs().max()).item())
-            out["sinc_gemm_ms"] = timeit(lambda: vad_model.conv1d_batched(x0, w0, None, 10))
-            out["conv2_gemm_ms"] = timeit(lambda: vad_model.conv1d_batched(x1, w1, b1, 1))
-            out["conv3_gemm_ms"] = timeit(lambda: vad_model.conv1d_batched(x2, w2, b2, 1))
         del x0, x1, x2
         torch.cuda.empty_cache()
+    if True:  # (the model is built outside inference_mode: its parameters must be normal tensors)
         from whisperx_amd.vad_model import VoiceActivitySegmentation
 
         torch.manual_seed(5)
@@ -71,7 +62,7 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    variants = {"default": {}, "gemm": {}, "no_gemm_solver": {"MIOPEN_DEBUG_CONV_GEMM": "0"},
+    variants = {"default": {}, "no_gemm_solver": {"MIOPEN_DEBUG_CONV_GEMM": "0"},
                 "find_normal": {"MIOPEN_FIND_MODE": "NORMAL"}}
     for tag, env in variants.items():
         e = dict(os.environ, **env)

@@ -107,9 +107,12 @@ _PATCH_BYTES = 1 << 30  # conv1d_batched: patch buffer per chunk of windows (Cin
 
 def conv1d_batched(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride: int) -> torch.Tensor:
     """F.conv1d(x, w, b, stride) (no padding, dilation 1, one group) for a batch of windows
-    through a few large GEMMs.  MIOpen runs these shapes as one im2col + GEMM per window
-    (21,573 im2col launches per hour of audio: half the producer's GPU time,
-    profiles/r3_vad1h_kernel_stats.csv).  Returns [B, Cout, Lout] as the transposed view of a
+    through a few large GEMMs.  MIOpen's choice for these shapes depends on the state of its
+    kernel cache: on a fresh MI355X box the first forward settles on one im2col + GEMM per
+    window for the whole process (21,573 im2col launches per hour of audio, half the producer's
+    GPU time: profiles/r3_vad1h_kernel_stats.csv; 1 h in 544 ms), on a warm one on an implicit
+    GEMM (200 ms).  These GEMMs take the same time either way (tools/vad_conv_probe.py: 14.4 /
+    7.9 / 2.8 ms per 2,048-window batch vs MIOpen's best 15.5 / 5.3 / 1.8 ms).  Returns [B, Cout, Lout] as the transposed view of a
     time-major [B, Lout, Cout] buffer.
 
     * Cin == 1 (the sinc filterbank, k = 251, stride 10): the taps are zero-padded to a multiple
@@ -176,7 +179,14 @@ class SincEncoder(torch.nn.Module):
         return self._cache[1]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _gemm_conv(x):
+            return conv1d_batched(x, self.weight(), None, self.stride)
         return F.conv1d(x, self.weight(), stride=self.stride)
+
+
+def _gemm_conv(x: torch.Tensor) -> bool:
+    """Inference forwards on a HIP device take conv1d_batched (WX_MIOPEN_CONV=1: MIOpen)."""
+    return x.is_cuda and not torch.is_grad_enabled() and not os.environ.get("WX_MIOPEN_CONV")
 
 
 class SincNet(torch.nn.Module):
@@ -195,7 +205,10 @@ class SincNet(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.wav_norm1d(x)
         for i, (conv, pool, norm) in enumerate(zip(self.conv1d, self.pool1d, self.norm1d)):
-            x = conv(x)
+            if i > 0 and _gemm_conv(x):
+                x = conv1d_batched(x, conv.weight, conv.bias, conv.stride[0])
+            else:
+                x = conv(x)
             if i == 0:
                 x = torch.abs(x)
             x = F.leaky_relu(norm(pool(x)))
