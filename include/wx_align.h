@@ -15,6 +15,8 @@
  *                        the kernel under vad.py:264 merge_chunks
  *   wx_channel_norm   <- whisperx/alignment.py:226-233 (wav2vec2 forward: feature encoder's
  *                        GroupNorm + GELU, time-major)
+ *   wx_attention_f32  <- whisperx/alignment.py:226-233 (wav2vec2 forward: the encoder's
+ *                        self-attention, fp32)
  *   wx_vad_aggregate  <- whisperx/vad.py:198-240 VoiceActivitySegmentation.apply's
  *                        segmentation overlap-add (pyannote Inference.aggregate)
  *
@@ -206,6 +208,16 @@ int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, i
 size_t wx_channel_norm_workspace_bytes(int32_t C);
 int wx_channel_norm(const float* x, int64_t L, int32_t C, const float* gamma, const float* beta, float eps,
                     int32_t gelu, float* y, void* workspace, size_t workspace_bytes, void* stream);
+
+/* wav2vec2 self-attention (alignment.py:226-233, the emission forward's encoder layers):
+ * o[b, t, h, :] = softmax(scale * q[b, h, t, :] . k[b, h, :, :]^T) v[b, h, :, :], fp32, no mask,
+ * head dim D = 64 only.  q/k/v are [B, H, T, 64] with element strides {batch, head, time}
+ * (*_strides[0..2]; the head dim is contiguous; rows 16-byte aligned) — transformers' views
+ * of the q/k/v projections need no copy; o is [B, T, H, 64] contiguous.  f32 MFMA, not
+ * bit-identical to torch's attention (different summation order). */
+int wx_attention_f32(const float* q, const float* k, const float* v, float* o, int32_t B, int32_t H, int32_t T,
+                     int32_t D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
+                     float scale, void* stream);
 
 /* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
  * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32

@@ -1,5 +1,6 @@
 """Emission producer kernels and routes (-m gpu): the time-major GroupNorm+GELU kernel
-against torch's fp32 GroupNorm + GELU, and the prepared (GEMM-conv + fused-norm) wav2vec2
+against torch's fp32 GroupNorm + GELU, the f32-MFMA attention against an fp64 attention, and
+the prepared (GEMM-conv + fused-norm + wx attention) wav2vec2
 forward against the stock PyTorch forward (fp32 reference of the same op; tolerance: the
 log-probabilities' float noise, with identical frame argmax)."""
 import numpy as np
@@ -35,6 +36,22 @@ def test_channel_norm_vs_torch_groupnorm(L, C, gelu):
     inplace = x.clone()
     _lib.channel_norm(inplace, g, b, gn.eps, gelu, out=inplace)
     assert torch.equal(inplace, got)
+
+
+@pytest.mark.parametrize("B,H,T", [(1, 12, 1), (1, 12, 31), (1, 12, 33), (1, 12, 400), (1, 12, 1499), (2, 16, 97)])
+def test_attention_f32_vs_fp64(B, H, T):
+    """wx_attention_f32 on transformers' q/k/v views of [B, T, H*64] projections against an
+    fp64 softmax(q k^T / 8) v; fp32 tolerance (f32 MFMA, its own summation order)."""
+    from whisperx_amd import _lib
+
+    torch.manual_seed(T)
+    proj = [torch.randn(B, T, H * 64, device="cuda") * 2 for _ in range(3)]
+    q, k, v = (p.view(B, T, H, 64).transpose(1, 2) for p in proj)  # [B, H, T, 64] views
+    got = _lib.attention_f32(q, k, v, 0.125)  # [B, T, H, 64]
+    qd, kd, vd = (x.double() for x in (q, k, v))
+    ref = torch.softmax(qd @ kd.transpose(-1, -2) * 0.125, -1) @ vd  # [B, H, T, 64]
+    ref = ref.transpose(1, 2).float()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
 
 
 def _check_prepared_vs_stock(m, V, lengths, tol=5e-5):

@@ -72,6 +72,7 @@ SIGNATURES = {
     "wx_channel_norm_workspace_bytes": (_sz, [_i32]),
     "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
+    "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
     "wx_binarize_workspace_bytes": (_sz, [_i32, _i64]),
@@ -480,6 +481,22 @@ def channel_norm(x: torch.Tensor, gamma, beta, eps: float, gelu: bool, out: Opti
         _check(lib.wx_channel_norm(_ptr(x), L, C, _ptr(gamma), _ptr(beta), float(eps), int(bool(gelu)), _ptr(y),
                                    _ptr(ws), ws.numel(), ctypes.c_void_p(stream.cuda_stream)))
     return y
+
+
+def attention_f32(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
+    """wx_attention_f32: softmax(scale * q k^T) v for [B, H, T, 64] fp32 device views (head dim
+    contiguous, any batch / head / time strides).  Returns [B, T, H, 64] (transformers'
+    attention-interface layout) on the current stream."""
+    lib = load()
+    B, H, T, D = (int(x) for x in q.shape)
+    if tuple(k.shape) != (B, H, T, D) or tuple(v.shape) != (B, H, T, D):
+        raise WXError(f"attention_f32: q/k/v shapes differ ({tuple(q.shape)}, {tuple(k.shape)}, {tuple(v.shape)})")
+    o = torch.empty((B, T, H, D), dtype=torch.float32, device=q.device)
+    st = [(ctypes.c_int64 * 3)(*(int(x) for x in t.stride()[:3])) for t in (q, k, v)]
+    with torch.cuda.device(q.device):
+        _check(lib.wx_attention_f32(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, T, D, st[0], st[1], st[2],
+                                    float(scale), _stream(q.device)))
+    return o
 
 
 class _StreamWorkspace(Workspace):

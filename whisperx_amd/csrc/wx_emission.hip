@@ -87,6 +87,186 @@ __global__ __launch_bounds__(256) void chan_apply_kernel(const float* __restrict
     reinterpret_cast<float4*>(y)[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// ------------------------------------------------------------------------------------
+// wav2vec2 self-attention, fp32 (alignment.py:226-233: the encoder's 12 / 24 attention layers,
+// one unpadded segment per forward, no mask).  torch's fused attention kernel for fp32
+// (aotriton attn_fwd) took 34% of config 3's GPU time at ~26 TFLOP/s (profiles/
+// r2_config3_kernel_stats.csv: 246 us per layer of a 29 s chunk).  Here: a flash-attention
+// forward on the f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 fmaf chains, 64 FLOP per
+// clock per SIMD), one workgroup per (batch, head, 32-query tile) whose kAttnSplit waves take
+// every kAttnSplit-th 32-key tile (a single 30 s segment has only 12 x 47 query tiles) and
+// merge their (max, sum, O) states through LDS at the end; per wave:
+//   * S^T = K Q^T per 32-key tile: lane l holds key row (l & 31) of K and query row (l & 31)
+//     of Q as the A / B operands; the head dimension is split 32 / 32 between the lane halves
+//     (the contraction order is free), so each lane reads contiguous 128-B half rows;
+//   * S^T's accumulator has the query on the lane and 16 keys per lane in registers, so the
+//     online softmax is lane-local plus one exchange with the other lane half, and the same
+//     registers are the B operand (P^T) of O^T += V^T P^T without any lane movement: MFMA j
+//     takes key (j & 3) + 8 (j >> 2) + 4 (l >> 5) from each half, and V is read at those rows;
+//   * O^T lives in two 32x32 accumulators (head dims 0-31, 32-63), rescaled lane-locally.
+// Not bit-identical to torch's kernel (different summation order); tests compare it with
+// torch's attention at fp32 tolerance and the whole prepared forward with the stock one.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct AttnArgs {
+    const float* q;
+    const float* k;
+    const float* v;
+    float* o;  // [B, T, H, 64]
+    int B, H, T;
+    int64_t sqb, sqh, sqt, skb, skh, skt, svb, svh, svt;  // element strides (head dim: 1)
+    float scale_log2;                                      // softmax scale * log2(e)
+};
+
+#ifndef WX_ATTN_SPLIT
+#define WX_ATTN_SPLIT 4
+#endif
+constexpr int kAttnSplit = WX_ATTN_SPLIT;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
+
+__global__ __launch_bounds__(64 * kAttnSplit) void attn_f32_kernel(AttnArgs a) {
+    const int T = a.T;
+    const int q0 = blockIdx.x * 32;
+    const int b = blockIdx.y / a.H, h = blockIdx.y % a.H;
+    const int l = threadIdx.x & 63, r = l & 31, hf = l >> 5, wv = threadIdx.x >> 6;
+    const float* Q = a.q + b * a.sqb + h * a.sqh;
+    const float* K = a.k + b * a.skb + h * a.skh;
+    const float* V = a.v + b * a.svb + h * a.svh;
+    float qv[32];
+    {
+        const float4* qp = reinterpret_cast<const float4*>(Q + (int64_t)min(q0 + r, T - 1) * a.sqt + 32 * hf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = qp[i];
+            qv[4 * i] = x.x;
+            qv[4 * i + 1] = x.y;
+            qv[4 * i + 2] = x.z;
+            qv[4 * i + 3] = x.w;
+        }
+    }
+    f32x16 o0, o1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
+    float m = -INFINITY, lsum = 0.f;
+    // K / V of the wave's next key tile are loaded while the current one computes
+    float kv[32], va[16], vb[16];  // K[key r][32 hf + j]; V[key(j)][r], V[key(j)][32 + r]
+    auto load_kv = [&](int k0, float(&kk)[32], float(&a0)[16], float(&a1)[16]) {
+        const float4* kp = reinterpret_cast<const float4*>(K + (int64_t)min(k0 + r, T - 1) * a.skt + 32 * hf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = kp[i];
+            kk[4 * i] = x.x;
+            kk[4 * i + 1] = x.y;
+            kk[4 * i + 2] = x.z;
+            kk[4 * i + 3] = x.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int key = min(k0 + (j & 3) + 8 * (j >> 2) + 4 * hf, T - 1);
+            const float* vr = V + (int64_t)key * a.svt;
+            a0[j] = vr[r];
+            a1[j] = vr[32 + r];
+        }
+    };
+    if (32 * wv < T) load_kv(32 * wv, kv, va, vb);
+    for (int k0 = 32 * wv; k0 < T; k0 += 32 * kAttnSplit) {
+        f32x16 s;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qv[j], s, 0, 0, 0);
+        float van[16], vbn[16];
+        {
+            const int kn = min(k0 + 32 * kAttnSplit, T - 1);  // (past the end: a harmless re-read)
+            load_kv(kn, kv, van, vbn);  // kv is dead once the S chain has been issued
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+            const float x = key < T ? s[i] * a.scale_log2 : -INFINITY;
+            s[i] = x;
+            mx = fmaxf(mx, x);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        float ps = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(s[i] - mn);
+            s[i] = p;
+            ps += p;
+        }
+        ps += __shfl_xor(ps, 32);
+        lsum = lsum * alpha + ps;
+        m = mn;
+        if (__any(alpha != 1.0f)) {  // (the running maximum settles after a few tiles)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                o0[i] *= alpha;
+                o1[i] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(va[j], s[j], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[j], s[j], o1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            va[j] = van[j];
+            vb[j] = vbn[j];
+        }
+    }
+    // merge the waves' partial softmax states (m, lsum, O^T) in wave 0
+    __shared__ float red[kAttnSplit - 1][34][64];
+    if (wv > 0) {
+        float* o = &red[wv - 1][0][l];
+        o[0] = m;
+        o[64] = lsum;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            o[64 * (2 + i)] = o0[i];
+            o[64 * (18 + i)] = o1[i];
+        }
+    }
+    __syncthreads();
+    if (wv > 0) return;
+    float mt = m;
+#pragma unroll
+    for (int w = 0; w < kAttnSplit - 1; ++w) mt = fmaxf(mt, red[w][0][l]);
+    {
+        const float c = __builtin_amdgcn_exp2f(m - mt);
+        lsum *= c;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            o0[i] *= c;
+            o1[i] *= c;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < kAttnSplit - 1; ++w) {
+        const float c = __builtin_amdgcn_exp2f(red[w][0][l] - mt);  // a wave without keys: 0
+        lsum += red[w][1][l] * c;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            o0[i] += red[w][2 + i][l] * c;
+            o1[i] += red[w][18 + i][l] * c;
+        }
+    }
+    if (q0 + r >= T) return;
+    const float inv = 1.0f / lsum;
+    float* orow = a.o + (((int64_t)b * T + q0 + r) * a.H + h) * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // registers 4g..4g+3: head dims 8g + 4hf + 0..3
+        const int d = 8 * g + 4 * hf;
+        *reinterpret_cast<float4*>(orow + d) =
+            make_float4(o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+        *reinterpret_cast<float4*>(orow + 32 + d) =
+            make_float4(o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    }
+}
+
 }  // namespace wxe
 
 extern "C" size_t wx_channel_norm_workspace_bytes(int32_t C) {
@@ -109,6 +289,44 @@ extern "C" int wx_channel_norm(const float* x, int64_t L, int32_t C, const float
     const int64_t n4 = L * (C / 4);
     hipLaunchKernelGGL(chan_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x, n4, C / 4, ab, C,
                        gelu, y);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, float* o, int32_t B, int32_t H,
+                                int32_t T, int32_t D, const int64_t* q_strides, const int64_t* k_strides,
+                                const int64_t* v_strides, float scale, void* stream) {
+    using namespace wxe;
+    if (B < 0 || H <= 0 || T < 0 || D != 64 || !q || !k || !v || !o || !q_strides || !k_strides || !v_strides)
+        return WX_E_INVALID;
+    if (B == 0 || T == 0) return WX_OK;
+    const int64_t* st[3] = {q_strides, k_strides, v_strides};
+    const float* pt[3] = {q, k, v};
+    for (int i = 0; i < 3; ++i) {  // 16-byte rows (float4 reads of Q / K)
+        if ((reinterpret_cast<uintptr_t>(pt[i]) & 15) || (st[i][0] & 3) || (st[i][1] & 3) || (st[i][2] & 3))
+            return WX_E_INVALID;
+    }
+    if (reinterpret_cast<uintptr_t>(o) & 15) return WX_E_INVALID;
+    AttnArgs a;
+    a.q = q;
+    a.k = k;
+    a.v = v;
+    a.o = o;
+    a.B = B;
+    a.H = H;
+    a.T = T;
+    a.sqb = q_strides[0];
+    a.sqh = q_strides[1];
+    a.sqt = q_strides[2];
+    a.skb = k_strides[0];
+    a.skh = k_strides[1];
+    a.skt = k_strides[2];
+    a.svb = v_strides[0];
+    a.svh = v_strides[1];
+    a.svt = v_strides[2];
+    a.scale_log2 = scale * 1.4426950408889634f;
+    hipLaunchKernelGGL(attn_f32_kernel, dim3((unsigned)((T + 31) / 32), (unsigned)(B * H)), dim3(64 * kAttnSplit), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

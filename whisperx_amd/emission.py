@@ -27,6 +27,10 @@ PyTorch-ROCm model call, one per segment, but:
   per channel, i.e. a per-channel normalisation over time) runs as the HIP kernel
   wx_channel_norm on the time-major conv output with the erf GELU fused, instead of torch's
   channel-major GroupNorm (which first copied the 96k x 512 activation).
+* **fp32 self-attention on the f32 MFMA.**  The encoder's attention layers go through
+  wx_attention_f32 (a flash-attention forward, one wave per 32-query tile; see
+  csrc/wx_emission.hip) via transformers' attention interface; torch's fused fp32 attention
+  was a third of config 3's GPU time.
 * **No concatenation copy.**  ``log_softmax`` writes each segment's ``[T, V]`` rows straight
   into its slice of the CSR emission matrix the DP kernel reads (``emissions_csr``).
 """
@@ -159,11 +163,52 @@ def _patched_forward(self, x):
     return self._wx_orig_forward(x)
 
 
+_ATTN_NAME = "wx_f32"
+
+
+def _wx_attention(module, query, key, value, attention_mask, dropout: float = 0.0, scaling=None, **kwargs):
+    """transformers attention interface (`config._attn_implementation = "wx_f32"`): the
+    encoder's unmasked fp32 self-attention of an inference forward on a HIP device through
+    wx_attention_f32 (f32 MFMA flash attention); anything else (masks, dropout, other dtypes
+    or head sizes, attention weights requested) through transformers' SDPA interface."""
+    if (query.is_cuda and attention_mask is None and not (dropout and module.training) and not torch.is_grad_enabled()
+            and not kwargs.get("output_attentions") and query.dtype == torch.float32 and query.shape[-1] == 64
+            and key.shape == query.shape and value.shape == query.shape and query.stride(-1) == 1
+            and key.stride(-1) == 1 and value.stride(-1) == 1):
+        from . import _lib
+
+        scale = scaling if scaling is not None else query.shape[-1] ** -0.5
+        return _lib.attention_f32(query, key, value, scale), None
+    from transformers.modeling_utils import ALL_ATTENTION_FUNCTIONS
+
+    return ALL_ATTENTION_FUNCTIONS["sdpa"](module, query, key, value, attention_mask, dropout=dropout,
+                                           scaling=scaling, **kwargs)
+
+
+def _use_wx_attention(model: torch.nn.Module) -> None:
+    """Point an HF model's attention interface at _wx_attention (WX_NO_ATTN=1: keep torch's)."""
+    cfg = getattr(model, "config", None)
+    if os.environ.get("WX_NO_ATTN") or cfg is None or not hasattr(cfg, "_attn_implementation"):
+        return
+    try:
+        from transformers import AttentionInterface
+        from transformers.modeling_utils import ALL_ATTENTION_FUNCTIONS
+
+        if _ATTN_NAME not in ALL_ATTENTION_FUNCTIONS:
+            AttentionInterface.register(_ATTN_NAME, _wx_attention)
+        orig = cfg._attn_implementation
+        cfg._attn_implementation = _ATTN_NAME
+        model._wx_orig_attn = orig
+    except Exception:  # an older transformers without the interface: torch's attention stays
+        pass
+
+
 def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
-    """Route the model's Conv1d inference forwards through length-agnostic GEMMs (idempotent).
-    Returns the same model object."""
+    """Route the model's Conv1d inference forwards through length-agnostic GEMMs and its
+    self-attention through wx_attention_f32 (idempotent).  Returns the same model object."""
     if getattr(model, "_wx_gemm_conv", False):
         return model
+    _use_wx_attention(model)
     for mod in model.modules():
         if isinstance(mod, torch.nn.Conv1d) and not hasattr(mod, "_wx_orig_forward"):
             mod._wx_orig_forward = mod.forward
@@ -189,6 +234,9 @@ def restore_model(model: torch.nn.Module) -> torch.nn.Module:
             del mod._wx_orig_forward
     if getattr(model, "_wx_gemm_conv", False):
         model._wx_gemm_conv = False
+    if hasattr(model, "_wx_orig_attn"):
+        model.config._attn_implementation = model._wx_orig_attn
+        del model._wx_orig_attn
     return model
 
 
