@@ -164,13 +164,9 @@ def mae_vs_oracle(ems_np, toks, plan):
     return mae, n_tok, n_bad_path
 
 
-def e2e_align(device, n_seg=16, seed=7):
-    """End-to-end align() on the GPU: random-weight wav2vec2-base (same architecture as
-    WAV2VEC2_ASR_BASE_960H) + fused DP + host aggregation, 30 s segments of synthetic
-    audio with ~14 chars/s transcripts."""
+def e2e_leg_inputs(device, n_seg=16, seed=7):
+    """e2e_align's inputs: (segments, audio, random-weight wav2vec2-base, align metadata)."""
     from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
-
-    import whisperx_amd
 
     torch.manual_seed(seed)
     model = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).to(device).eval()
@@ -183,6 +179,16 @@ def e2e_align(device, n_seg=16, seed=7):
         words = ["".join(rng.choice(list(letters), int(rng.integers(2, 9)))) for _ in range(70)]
         segs.append({"start": 30.0 * k, "end": 30.0 * (k + 1), "text": " ".join(words)})
     audio = torch.from_numpy(rng.standard_normal(int(30 * n_seg * 16000)).astype(np.float32) * 0.1)
+    return segs, audio, model, meta
+
+
+def e2e_align(device, n_seg=16, seed=7):
+    """End-to-end align() on the GPU: random-weight wav2vec2-base (same architecture as
+    WAV2VEC2_ASR_BASE_960H) + fused DP + host aggregation, 30 s segments of synthetic
+    audio with ~14 chars/s transcripts."""
+    import whisperx_amd
+
+    segs, audio, model, meta = e2e_leg_inputs(device, n_seg, seed)
     whisperx_amd.align([dict(s) for s in segs[:2]], model, meta, audio, device)  # warm-up
     torch.cuda.synchronize()
     st0 = _dp_stats()

@@ -44,6 +44,23 @@ def main():
         torch.cuda.synchronize()
         print(f"vad1h: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, 1 h of audio", flush=True)
         return
+    if a.leg == "e2e":  # align() end to end on 16 x 30 s segments (bench.e2e_align's inputs)
+        import bench
+
+        segs, audio, model, meta = bench.e2e_leg_inputs(dev)
+        import whisperx_amd
+
+        for _ in range(max(1, a.warmup)):
+            whisperx_amd.align(segs, model, meta, audio, dev)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.steps):
+            whisperx_amd.align(segs, model, meta, audio, dev)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"e2e: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, {len(segs)} segments", flush=True)
+        return
     if a.leg == "cfg2":
         ems, toks = make_batch(64, 1499, 32, 300, 500, 1000, dev)
     else:
