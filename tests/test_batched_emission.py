@@ -25,6 +25,7 @@ def test_batched_logits_match_per_segment_forward(monkeypatch, stable):
     from whisperx_amd import _lib, emission
 
     monkeypatch.setattr(_lib, "attention_f32_csr", _torch_attention_csr)
+    monkeypatch.setenv("WX_EMISSION_BATCH", "8")
     torch.manual_seed(0)
     if stable:
         cfg = Wav2Vec2Config(vocab_size=40, num_hidden_layers=2, hidden_size=256, num_attention_heads=4,

@@ -170,9 +170,9 @@ def test_emissions_fan_out_fresh_parametrised_model(monkeypatch, batched):
     from whisperx_amd import alignment, emission
 
     if batched:
-        monkeypatch.delenv("WX_NO_BATCH", raising=False)
+        monkeypatch.setenv("WX_EMISSION_BATCH", "8")
     else:
-        monkeypatch.setenv("WX_NO_BATCH", "1")
+        monkeypatch.delenv("WX_EMISSION_BATCH", raising=False)
     torch.manual_seed(2)
     m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
     pos = m.wav2vec2.encoder.pos_conv_embed.conv

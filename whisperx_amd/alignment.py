@@ -317,7 +317,7 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     if model_type == "huggingface" and emission.batchable(model):
         # batched forwards (emission.batched_logits): WX_EMISSION_BATCH segments per group, the
         # groups round-robin on the streams; one event per group
-        G = max(1, int(os.environ.get("WX_EMISSION_BATCH", "8")))
+        G = max(1, int(os.environ.get("WX_EMISSION_BATCH", "8")))  # (batchable: > 0)
         for g0 in range(0, len(waveforms), G):
             st = streams[(g0 // G) % len(streams)]
             with torch.cuda.stream(st):

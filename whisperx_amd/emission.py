@@ -241,12 +241,17 @@ def restore_model(model: torch.nn.Module) -> torch.nn.Module:
 
 
 def batchable(model) -> bool:
-    """Whether batched_logits can run `model`: an HF Wav2Vec2ForCTC (base / post-norm or
-    stable-layer-norm encoder, no adapter) with 64-wide heads, in eval mode, unless
-    WX_NO_BATCH=1."""
+    """Whether align() runs `model` through batched_logits: opt-in (WX_EMISSION_BATCH=G > 0,
+    G segments per batch), for an HF Wav2Vec2ForCTC (base / post-norm or stable-layer-norm
+    encoder, no adapter) with 64-wide heads, in eval mode.  Off by default: on MI355X the
+    per-segment forwards on 8 streams already overlap enough that batching gains nothing
+    (16 x 30 s, steady state: 105.9 ms per-segment vs 104.8-120.1 ms batched at G = 16..2;
+    config 3 slower at G = 8), the fp32 matrix work being the bound."""
     w2v = getattr(model, "wav2vec2", None)
     cfg = getattr(model, "config", None)
-    if os.environ.get("WX_NO_BATCH") or w2v is None or cfg is None or model.training:
+    if int(os.environ.get("WX_EMISSION_BATCH", "0") or 0) <= 0 or os.environ.get("WX_NO_BATCH"):
+        return False
+    if w2v is None or cfg is None or model.training:
         return False
     enc = getattr(w2v, "encoder", None)
     if enc is None or getattr(w2v, "adapter", None) is not None or not hasattr(model, "lm_head"):
