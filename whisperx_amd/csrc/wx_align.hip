@@ -54,6 +54,9 @@ constexpr int kUnroll = 8;  // time steps per unrolled group
 #ifndef WX_C8_UNROLL
 #define WX_C8_UNROLL 8  // ... for C >= 8 non-pipelined waves (Forward::kU; 4: A/B neutral)
 #endif
+#ifndef WX_COUNTED_WAIT
+#define WX_COUNTED_WAIT 0  // chunk-boundary wait skips the previous chunk's bitmap stores (A/B knob)
+#endif
 constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
 __device__ __forceinline__ float nan_max(float a, float b) {
@@ -285,6 +288,11 @@ __device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, i
 }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// all but the N most recent vector memory operations of this wave (they complete in order)
+template <int N>
+__device__ __forceinline__ void wait_vm_but() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 __device__ __forceinline__ void wave_fence() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -473,6 +481,7 @@ struct Forward {
     static constexpr bool kReg = false;
 #endif
     static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
+    static constexpr bool kCountedWait = WX_COUNTED_WAIT && MODE == 0 && !SP;
     static constexpr int kQS = quad_stride<VS>();
 
     // Per-lane state of the forward pass.
@@ -665,7 +674,15 @@ struct Forward {
                 for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
             }
             WX_T(c1);
-            if (!H) wait_vm();  // this wave's staging (with a helper, DP waves stage nothing)
+            // this wave's staging (with a helper, DP waves stage nothing).  Single-CU fused
+            // launches: not the previous chunk's C bitmap stores, issued last (the wait would
+            // expose a store round trip per chunk)
+            if (!H) {
+                if (kCountedWait && q > 0)
+                    wait_vm_but<C>();
+                else
+                    wait_vm();
+            }
             __syncthreads();
             WX_T(c2);
             if (W > 1 && q > 0 && halo && wv > 0) {
