@@ -57,6 +57,9 @@ constexpr int kUnroll = 8;  // time steps per unrolled group
 #ifndef WX_COUNTED_WAIT
 #define WX_COUNTED_WAIT 0  // chunk-boundary wait skips the previous chunk's bitmap stores (A/B knob)
 #endif
+#ifndef WX_PIPE_C8W
+#define WX_PIPE_C8W 0  // A/B knob: software-pipelined operands in the multi-wave C = 8 buckets (no gain)
+#endif
 constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
 __device__ __forceinline__ float nan_max(float a, float b) {
@@ -464,7 +467,7 @@ struct Forward {
     // Software-pipelined LDS operands where the extra registers keep the occupancy that
     // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
-    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
+    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && (W == 1 || WX_PIPE_C8W))));
     using Geo = Geometry<C, (SP ? 2 : W)>;  // SP: always a halo (the waves span P parts)
     // Steps per unrolled group of the non-pipelined chunk (hipcc hoists the group's LDS
     // loads; a multiple of 4: column-N history is stored as float4).
@@ -2239,7 +2242,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 }
 
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu((WX_PIPE_C8W && C == 8 && W > 1 && !H && VS != kGatherVS) ? 4 : 1, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
 }
