@@ -102,7 +102,7 @@ class SincFilterbank(torch.nn.Module):
         return torch.cat(out, dim=0)
 
 
-_PATCH_BYTES = 1 << 30  # conv1d_batched: patch buffer per chunk of windows (Cin == 1)
+_PATCH_BYTES = int(os.environ.get("WX_VAD_PATCH_MB", "1024")) << 20  # conv1d_batched: patch buffer per chunk of windows (Cin == 1)
 
 
 def conv1d_batched(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride: int) -> torch.Tensor:
