@@ -634,6 +634,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1
+    pin = None
+    if dist_on:  # disjoint host CPUs per rank, before any GPU call
+        from whisperx_amd.distributed import pin_rank
+
+        pin = pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+        log(f"bench[{rank}]: pinned to {len(pin['cpus'] or [])} CPUs, {pin['threads']} torch threads")
     # one GPU per rank (LOCAL_RANK); WX_DIST_BACKEND=gloo rehearses the multi-rank path on a
     # box with fewer GPUs than ranks (ranks then share GPUs; RCCL refuses that)
     backend = os.environ.get("WX_DIST_BACKEND", "nccl")
@@ -700,7 +706,9 @@ def main():
             "config": {"workload": "cfg2: batch=64 x 30 s EN segments, T=1499, V=32, N~U[300,500]; "
                                    "fused HIP align DP (wx_align_dp) on HBM-resident emissions",
                        "global_batch": args.segments * world, "seq_len": T,
-                       "parallelism": f"dp{world} (per-file sharding, RCCL vocab broadcast)"},
+                       "parallelism": f"dp{world} (per-file sharding, RCCL vocab broadcast)"
+                                      + (f"; host pinning: {pin['threads']} threads per rank on disjoint CPUs"
+                                         if pin else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname + (" (the step's only launch)" if len(knames) == 1 else
@@ -850,11 +858,9 @@ def main():
 
 
 def _host_threads():
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(n, 1)
+    from whisperx_amd.distributed import thread_budget
+
+    return thread_budget()
 
 
 def _cpu_model():

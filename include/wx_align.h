@@ -200,6 +200,13 @@ int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, i
                    double* reg_start, double* reg_end, const int64_t* reg_off, int64_t* reg_count,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* Diagnostics (no device work): the kernels wx_binarize_ex launches for these thresholds
+ * (compared in fp32, as wx_binarize_ex does), ';'-separated rocprof names written to buf
+ * (truncated to n bytes).  offset <= onset takes the parallel scan, offset > onset (a frame
+ * may both set and reset the state, vad.py:146-175) the event-jumping state machine.
+ * Returns their number. */
+int wx_binarize_plan(float onset, float offset, int64_t total_frames, char* buf, size_t n);
+
 /* Emission producer (alignment.py:226-233, the wav2vec2 forward): GroupNorm with one group
  * per channel (the first feature-encoder layer) over time-major activations x [L, C] (C % 4
  * == 0, 16-byte aligned), with the affine gamma/beta (may be NULL) and, when gelu != 0, the

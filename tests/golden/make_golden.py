@@ -487,11 +487,43 @@ def build_vad_cases(Vd, pc):
     sw = pc.SlidingWindow(start=0.0, step=STEP, duration=DUR)
     ann = Vd.Binarize(onset=0.5, offset=0.363, min_duration_on=0.25)(pc.SlidingWindowFeature(sc[:, None], sw))
     expected_min = [[s.start, s.end] for s, _t in ann.itertracks()]
+    # offset > onset (transcribe.py:42-43 --vad_onset/--vad_offset): a frame can both set and
+    # reset the hysteresis state (vad.py:146-175).  Own generator, so the cases above keep
+    # their scores.
+    rng2 = np.random.default_rng(4242)
+    specs2 = [
+        (5000, 40, 0.0, 0.4, 0.6, 30, 0.0),
+        (5000, 40, 0.0, 0.5, 0.55, 30, 0.0),
+        (4000, 30, 0.0, 0.4, 0.6, 1, 0.0),
+        (4000, 30, 0.0, 0.5, 0.55, 1, 0.0),
+        (35556, 80, 3.0, 0.4, 0.6, 30, 0.0),    # mostly speech: min-cut splits
+        (35556, 80, 3.0, 0.5, 0.55, 30, 0.125),
+        (20000, 60, 0.5, 0.45, 0.7, 10, 0.25),
+        (3000, 40, 9.0, 0.4, 0.6, 1, 0.0),      # all speech, a cut every second
+        (3000, 20, 0.0, 0.3, 0.9, 5, 0.0),
+    ]
+    base = len(specs)
+    for k, (F, smooth, bias, onset, offset, chunk, sw0) in enumerate(specs2):
+        ci = base + k
+        sc = vad_scores(rng2, F, smooth, bias)
+        if k == 0:  # exact threshold ties
+            sc[::83] = np.float32(0.4)
+            sc[7::71] = np.float32(0.6)
+        sw = pc.SlidingWindow(start=sw0, step=STEP, duration=DUR)
+        feat = pc.SlidingWindowFeature(sc[:, None], sw)
+        ann = Vd.Binarize(max_duration=chunk, onset=onset, offset=offset)(feat)
+        chunks = Vd.merge_chunks(feat, chunk, onset=onset, offset=offset)
+        arrays[f"v{ci:02d}_scores"] = sc
+        expected.append({"F": F, "onset": onset, "offset": offset, "chunk_size": chunk,
+                         "sw_start": sw0, "sw_step": STEP, "sw_duration": DUR,
+                         "regions": [[s.start, s.end] for s in ann.get_timeline()],
+                         "chunks": [{"start": c["start"], "end": c["end"],
+                                     "segments": [list(p) for p in c["segments"]]} for c in chunks]})
     np.savez_compressed(os.path.join(OUT, "vad_cases.npz"), **arrays)
     with open(os.path.join(OUT, "vad_cases.json"), "w") as f:
         json.dump({"cases": expected, "min_duration_on": {"onset": 0.5, "offset": 0.363,
                    "min_duration_on": 0.25, "regions": expected_min}}, f, indent=0)
-    print("vad cases:", len(specs) + 1)
+    print("vad cases:", len(specs) + len(specs2) + 1)
 
 
 if __name__ == "__main__":

@@ -111,3 +111,17 @@ def test_product_refuses_without_device():
         pytest.skip("a device is visible")
     with pytest.raises(_lib.WXError):
         _lib.load(require_device=True)
+
+
+def test_binarize_plan_kernel_selection(lib):
+    """wx_binarize_plan (no device work): offset <= onset takes the parallel scan, offset >
+    onset (vad.py:146-175: a frame may both set and reset) the event-jumping state machine."""
+    from whisperx_amd import _lib
+
+    words = "void wx::binarize_words_kernel(wx::BinWordArgs)"
+    scan = "void wx::binarize_scan_kernel(wx::BinScanArgs)"
+    fsm = "void wx::binarize_fsm_kernel(wx::BinarizeArgs, wx::BinWords)"
+    assert _lib.binarize_plan(0.5, 0.363, 1000) == [words, scan]
+    assert _lib.binarize_plan(0.5, 0.5, 1000) == [words, scan]
+    assert _lib.binarize_plan(0.4, 0.6, 1000) == [words, fsm]
+    assert _lib.binarize_plan(0.5, 0.55, 0) == [fsm]

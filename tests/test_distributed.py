@@ -8,7 +8,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from whisperx_amd.distributed import (_decode_dictionary, _encode_dictionary, align_corpus,
-                                      broadcast_dictionary, gather_results, shard_files)
+                                      broadcast_dictionary, gather_results, pin_rank, rank_cpus, shard_files)
 
 
 def test_shard_files_lpt_balanced_and_complete():
@@ -38,6 +38,20 @@ def test_dictionary_codec_roundtrip():
     assert _decode_dictionary(_encode_dictionary(d)) == d
 
 
+def test_rank_cpus_disjoint_and_covering():
+    for cpus in ([0, 1, 2, 3, 4, 5, 6, 7], list(range(16)), [3, 9, 12], list(range(0, 256, 2))):
+        for world in (1, 2, 3, 4, 8):
+            parts = [rank_cpus(cpus, r, world) for r in range(world)]
+            if world <= len(cpus):
+                assert sorted(c for p in parts for c in p) == sorted(cpus)
+                assert all(p for p in parts)
+                assert max(map(len, parts)) - min(map(len, parts)) <= 1
+            else:
+                assert all(len(p) == 1 for p in parts)
+    with pytest.raises(ValueError):
+        rank_cpus([0, 1], 2, 2)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -49,13 +63,16 @@ def _free_port():
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    pin = pin_rank(rank, world)  # before anything else, as bench.py's ranks do
+    pin["affinity"] = sorted(os.sched_getaffinity(0))
+    pin["torch_threads"] = torch.get_num_threads()
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         vocab = {"<pad>": 0, "|": 4, "e": 5, "t": 6, "ä": 33} if rank == 0 else None
         got = broadcast_dictionary(vocab, device=None)
         durs = [30.0, 10.0, 25.0, 5.0, 60.0]
         res = align_corpus([f"f{i}" for i in range(5)], lambda f: {"file": f, "rank": rank}, durs)
-        q.put((rank, got, res))
+        q.put((rank, got, res, pin))
     finally:
         dist.destroy_process_group()
 
@@ -72,8 +89,17 @@ def test_gloo_world2_broadcast_and_gather():
         p.join(timeout=60)
         assert p.exitcode == 0
     outs.sort(key=lambda x: x[0])
-    for rank, got, res in outs:
+    for rank, got, res, pin in outs:
         assert got == {"<pad>": 0, "|": 4, "e": 5, "t": 6, "ä": 33}
+    # per-rank host pinning: disjoint CPU sets covering the parent's affinity, pools sized to them
+    parent = sorted(os.sched_getaffinity(0))
+    sets = [o[3]["affinity"] for o in outs]
+    if len(parent) >= 2:
+        assert not set(sets[0]) & set(sets[1])
+        assert sorted(sets[0] + sets[1]) == parent
+    for o in outs:
+        assert o[3]["affinity"] == o[3]["cpus"]
+        assert 1 <= o[3]["torch_threads"] <= len(o[3]["cpus"])
     merged = outs[0][2]
     assert outs[1][2] is None
     assert sorted(merged) == [0, 1, 2, 3, 4]

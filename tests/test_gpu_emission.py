@@ -192,3 +192,140 @@ def test_emissions_fan_out_fresh_parametrised_model(monkeypatch, batched):
             assert err <= (5e-5 if batched else 1e-6), f"segment {i}: fan-out emission differs from single-stream by {err}"
             assert torch.equal(csr[i].argmax(-1), ref.argmax(-1))
     emission.restore_model(m)
+
+
+# --------------------------------------------------------------- torchaudio-shaped models
+class _TAConvBlock(torch.nn.Module):
+    """torchaudio's ConvLayerBlock shape: conv -> optional norm -> F.gelu, lengths tracked."""
+
+    def __init__(self, cin, cout, k, s, norm):
+        super().__init__()
+        self.kernel_size, self.stride = k, s
+        self.conv = torch.nn.Conv1d(cin, cout, k, s, bias=False)
+        self.layer_norm = norm
+
+    def forward(self, x, length):
+        x = self.conv(x)
+        if self.layer_norm is not None:
+            x = self.layer_norm(x)
+        x = torch.nn.functional.gelu(x)
+        if length is not None:
+            length = torch.clamp(torch.div(length - self.kernel_size, self.stride, rounding_mode="floor") + 1, min=0)
+        return x, length
+
+
+class _TAPosConv(torch.nn.Module):
+    """torchaudio's ConvolutionalPositionalEmbedding: grouped weight-normed conv (dim=2),
+    padding k // 2, the last frame dropped for an even kernel, GELU."""
+
+    def __init__(self, d, k, groups, parametrized):
+        super().__init__()
+        conv = torch.nn.Conv1d(d, d, k, padding=k // 2, groups=groups)
+        if parametrized:
+            conv = torch.nn.utils.parametrizations.weight_norm(conv, name="weight", dim=2)
+        else:
+            conv = torch.nn.utils.weight_norm(conv, name="weight", dim=2)  # the older hook form
+        self.conv = conv
+        self.num_remove = 1 if k % 2 == 0 else 0
+
+    def forward(self, x):
+        x = self.conv(x.transpose(-2, -1))
+        if self.num_remove > 0:
+            x = x[..., : -self.num_remove]
+        return torch.nn.functional.gelu(x).transpose(-2, -1)
+
+
+class _TAWav2Vec2(torch.nn.Module):
+    """A torchaudio-bundle-shaped wav2vec2 (WAV2VEC2_ASR_BASE_960H layout at reduced depth):
+    feature_extractor(ConvLayerBlocks) -> projection -> positional conv -> transformer layers
+    -> aux head; forward(x, lengths) -> (emissions, lengths) as alignment.py:227-228 calls it."""
+
+    def __init__(self, V=29, d=768, layers=2, parametrized=True):
+        super().__init__()
+        shapes = [(1, 512, 10, 5)] + [(512, 512, 3, 2)] * 4 + [(512, 512, 2, 2)] * 2
+        self.feature_extractor = torch.nn.ModuleList(
+            [_TAConvBlock(ci, co, k, s, torch.nn.GroupNorm(512, 512) if i == 0 else None)
+             for i, (ci, co, k, s) in enumerate(shapes)])
+        self.proj_norm = torch.nn.LayerNorm(512)
+        self.proj = torch.nn.Linear(512, d)
+        self.pos_conv = _TAPosConv(d, 128, 16, parametrized)
+        self.norm = torch.nn.LayerNorm(d)
+        self.layers = torch.nn.ModuleList(
+            [torch.nn.TransformerEncoderLayer(d, 12, 3072, dropout=0.0, activation="gelu", batch_first=True)
+             for _ in range(layers)])
+        self.aux = torch.nn.Linear(d, V)
+
+    def forward(self, x, lengths=None):
+        x = x.unsqueeze(1)
+        for blk in self.feature_extractor:
+            x, lengths = blk(x, lengths)
+        x = self.proj(self.proj_norm(x.transpose(1, 2)))
+        x = self.norm(x + self.pos_conv(x))
+        for layer in self.layers:
+            x = layer(x)
+        return self.aux(x), lengths
+
+
+@pytest.mark.parametrize("parametrized", [True, False])
+def test_torchaudio_shaped_model_prepared_vs_stock(parametrized):
+    """alignment.py:227-228's torchaudio branch through the emission route: a stand-in with
+    torchaudio's module layout (ConvLayerBlock convs, weight-norm positional conv in both the
+    parametrisation and the older hook form, aux head, (emissions, lengths) output) gives the
+    same log-probabilities as its unprepared forward (<= 5e-5, identical frame argmax), for a
+    < 400-sample segment (padded, lengths passed) too.  torchaudio itself is absent here, so
+    parity with the real bundles is unpinned."""
+    from whisperx_amd import alignment, emission
+
+    torch.manual_seed(5)
+    m = _TAWav2Vec2(parametrized=parametrized).cuda().eval()
+    g = torch.Generator().manual_seed(6)
+    wavs = [(torch.randn(1, n, generator=g) * 0.1).cuda() for n in (30 * 16000, 123457, 300, 400)]
+    with torch.inference_mode():
+        ref = [torch.log_softmax(alignment._logits(m, "torchaudio", w, "cuda:0"), -1)[0] for w in wavs]
+    with emission.prepared(m):
+        csr = alignment._emissions(m, "torchaudio", wavs, "cuda:0", n_streams=4)
+        assert isinstance(csr, alignment._EmissionsCSR), "the torchaudio branch left the packed emission route"
+        main = torch.cuda.current_stream()
+        for st in csr.streams:
+            main.wait_stream(st)
+        torch.cuda.synchronize()
+        got = [csr[i].clone() for i in range(len(wavs))]
+        assert any("forward" in mod.__dict__ for mod in m.modules()), "no convolution took the GEMM route"
+    for i, (a, b) in enumerate(zip(got, ref)):
+        assert a.shape == b.shape, (i, a.shape, b.shape)
+        err = float((a - b).abs().max())
+        assert err <= 5e-5, f"segment {i}: max |prepared - stock| = {err}"
+        assert torch.equal(a.argmax(-1), b.argmax(-1)), f"segment {i}: frame argmax differs"
+    # the caller's model is unchanged afterwards
+    assert not any("forward" in mod.__dict__ or hasattr(mod, "_wx_w_cache") for mod in m.modules())
+
+
+def test_align_leaves_callers_model_unchanged():
+    """align() prepares the model for the call only (alignment.py:226-233 takes the caller's
+    model and leaves it alone): afterwards no instance-level forwards, no cached weights, the
+    original attention implementation, identical state_dict, and the stock forward's output."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    from whisperx_amd import align
+
+    torch.manual_seed(7)
+    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32, num_hidden_layers=2)).cuda().eval()
+    attn0 = m.config._attn_implementation
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    x = (torch.randn(1, 5 * 16000, generator=torch.Generator().manual_seed(8)) * 0.1).cuda()
+    with torch.inference_mode():
+        y0 = m(x).logits.clone()
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    dictionary = {c: i + 4 for i, c in enumerate(letters)}
+    dictionary.update({"<pad>": 0, "|": 1})
+    segs = [{"start": 0.0, "end": 2.5, "text": "hello world"}, {"start": 2.5, "end": 5.0, "text": "again here"}]
+    out = align(segs, m, {"language": "en", "dictionary": dictionary, "type": "huggingface"}, x[0], "cuda:0")
+    assert len(out["segments"]) == 2
+    assert m.config._attn_implementation == attn0
+    assert not any("forward" in mod.__dict__ or hasattr(mod, "_wx_w_cache") or hasattr(mod, "_wx_orig_forward")
+                   for mod in m.modules())
+    assert not hasattr(m, "_wx_gemm_conv") and not hasattr(m, "_wx_orig_attn")
+    sd1 = m.state_dict()
+    assert sd0.keys() == sd1.keys() and all(torch.equal(sd0[k], sd1[k]) for k in sd0)
+    with torch.inference_mode():
+        assert torch.equal(m(x).logits, y0)

@@ -59,7 +59,7 @@ def test_align_dp_matches_reference_golden(dp_cases):
         for s, (i, c) in enumerate(items):
             assert ts[s] == int(c["t_start"]), f"case {i}: t_start {ts[s]} != {int(c['t_start'])}"
             ok = int(c["path_ok"]) == 1
-            assert st[s] == (0 if ok else 1), f"case {i}: status {st[s]}"
+            assert (st[s] & _lib.STATUS_MASK) == (0 if ok else 1), f"case {i}: status {st[s]}"
             if not ok:
                 continue
             a, e = b.tok_off[s], b.tok_off[s + 1]
@@ -123,6 +123,60 @@ def test_align_dp_random_mixed_buckets_vs_oracle(V, mode):
     cases += _random_cases(rng, 6, (20, 300), (1, 60), V, quant=16)  # exact ties
     cases += _random_cases(rng, 4, (5, 40), (20, 60), V)  # N > T: backtrack fails
     _check_vs_oracle(cases, f"V{V} mode {mode}", mode)
+
+
+def test_align_dp_concurrent_streams_vs_oracle():
+    """The wrapper is as reentrant as the ABI: align_dp batches enqueued back to back on two
+    streams (and from two threads) without a sync between them each use their own workspace
+    and hand-off region (keyed by (device, stream)), and each equals the oracle."""
+    import threading
+
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(77)
+    sets = [_random_cases(rng, 24, (1200, 1500), (300, 500), 32),   # split launch (4 CUs each)
+            _random_cases(rng, 300, (200, 700), (20, 200), 32),     # throughput buckets
+            _random_cases(rng, 40, (900, 1500), (100, 400), 29)]
+    batches = [_batch(c) for c in sets]
+    streams = [torch.cuda.Stream(device=DEV) for _ in batches]
+    torch.cuda.synchronize()
+    want = [[oracle.align_dp(c["em"], c["tokens"], int(c["blank"])) for c in cases] for cases in sets]
+
+    def check(outs, tag):
+        for k, (b, out) in enumerate(zip(batches, outs)):
+            ss, se, sc, ts, st = (x.cpu().numpy() for x in out)
+            for s, (ok, tso, sso, seo, sco) in enumerate(want[k]):
+                assert ts[s] == tso and bool(_lib.status_ok(st[s])) == ok, f"{tag} batch {k} seg {s}"
+                if ok:
+                    a, e = b.tok_off[s], b.tok_off[s + 1]
+                    assert np.array_equal(ss[a:e], sso) and np.array_equal(se[a:e], seo), f"{tag} {k}/{s}: spans"
+                    assert np.allclose(sc[a:e], sco, rtol=1e-12, atol=0, equal_nan=True), f"{tag} {k}/{s}: scores"
+
+    outs = [None] * len(batches)
+    for rep in range(3):
+        for i, (b, st) in enumerate(zip(batches, streams)):
+            with torch.cuda.stream(st):
+                outs[i] = _lib.align_dp(b)
+        torch.cuda.synchronize()
+        check(outs, f"streams rep {rep}")
+        errs = []
+
+        def run(i):
+            try:
+                with torch.cuda.stream(streams[i]):
+                    outs[i] = _lib.align_dp(batches[i])
+                streams[i].synchronize()
+            except Exception as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(len(batches))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        torch.cuda.synchronize()
+        check(outs, f"threads rep {rep}")
 
 
 def _skewed_cases(rng, V=32):
@@ -546,15 +600,22 @@ def _vad():
 def test_binarize_and_merge_chunks_match_reference():
     from whisperx_amd.vad import Binarize, SlidingWindow, SlidingWindowFeature, merge_chunks
 
+    from whisperx_amd import _lib
+
     meta, arr = _vad()
+    kernels = set()
     for ci, c in enumerate(meta["cases"]):
         sc = arr[f"v{ci:02d}_scores"]
+        kernels.add(_lib.binarize_plan(c["onset"], c["offset"] if c["offset"] is not None else c["onset"])[-1])
         feat = SlidingWindowFeature(sc[:, None], SlidingWindow(c["sw_start"], c["sw_step"], c["sw_duration"]))
         ann = Binarize(max_duration=c["chunk_size"], onset=c["onset"], offset=c["offset"])(feat)
         assert [[s.start, s.end] for s in ann.get_timeline()] == c["regions"], f"vad case {ci}"
         chunks = merge_chunks(feat, c["chunk_size"], onset=c["onset"], offset=c["offset"])
         got = [{"start": x["start"], "end": x["end"], "segments": [list(p) for p in x["segments"]]} for x in chunks]
         assert got == c["chunks"], f"vad case {ci}"
+    # the golden cases reach both wx_binarize_ex routes (offset > onset since round 4)
+    assert kernels == {"void wx::binarize_scan_kernel(wx::BinScanArgs)",
+                       "void wx::binarize_fsm_kernel(wx::BinarizeArgs, wx::BinWords)"}
     m = meta["min_duration_on"]
     sc = arr["vmin_scores"]
     feat = SlidingWindowFeature(sc[:, None], SlidingWindow(0.0, 0.016875, 0.0619375))
@@ -595,10 +656,14 @@ def _binarize_both(cols, geom, onset, offset, maxd):
 
 
 def test_binarize_dense_events_nan_and_ragged_files():
-    """The two-pass kernel (bit-word pre-pass + event-jumping state machine) and the one-pass
-    scan against the oracle where every other frame is an event (noise thresholded at its
-    median), min-cuts span many 64-frame blocks, blocks hold NaNs (np.argmin takes the first
-    NaN), and files are 0, 1, 2, 63, 64, 65 ... frames long (partial words, words of one frame)."""
+    """wx_binarize_ex (bit-word pre-pass, then the parallel scan for offset <= onset or the
+    event-jumping state machine binarize_fsm_kernel for offset > onset — the plan is asserted
+    per pair) and the one-pass scan wx_binarize, against the oracle, where every other frame
+    is an event (noise thresholded near its median), min-cuts span many 64-frame blocks, blocks
+    hold NaNs (np.argmin takes the first NaN), and files are 0, 1, 2, 63, 64, 65 ... frames
+    long (partial words, words of one frame)."""
+    from whisperx_amd import _lib
+
     rng = np.random.default_rng(11)
     lens = [0, 1, 2, 63, 64, 65, 127, 128, 129, 1000, 4095, 4096, 4097, 0, 9000, 30001]
     cols = []
@@ -610,8 +675,15 @@ def test_binarize_dense_events_nan_and_ragged_files():
             y = np.round(y * 8) / 8
         cols.append(y)
     geom = [(0.1 * i, 0.016875, 0.0619375) for i in range(len(cols))]
+    scan = "void wx::binarize_scan_kernel(wx::BinScanArgs)"
+    fsm = "void wx::binarize_fsm_kernel(wx::BinarizeArgs, wx::BinWords)"
     for onset, offset, maxd in ((0.5, 0.5, 30.0), (0.5, 0.363, 1.0), (0.2, 0.1, 0.5), (0.95, 0.9, 0.05),
-                                (0.5, 0.4, float("inf")), (0.0, 0.0, 2.0)):
+                                (0.5, 0.4, float("inf")), (0.0, 0.0, 2.0),
+                                # offset > onset: binarize_fsm_kernel
+                                (0.4, 0.6, 30.0), (0.5, 0.55, 1.0), (0.3, 0.9, 0.5), (0.45, 0.5, float("inf")),
+                                (0.0, 1.0, 2.0), (0.5, 0.5000001, 0.05)):
+        want = fsm if np.float32(offset) > np.float32(onset) else scan
+        assert _lib.binarize_plan(onset, offset, sum(len(c) for c in cols))[-1] == want, (onset, offset)
         _binarize_both(cols, geom, onset, offset, maxd)
 
 

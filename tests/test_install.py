@@ -54,6 +54,14 @@ SCRIPT = textwrap.dedent(r'''
     ref_align = whisperx.transcribe.align
     assert ref_align is whisperx.alignment.align          # before: the reference CPU path
 
+    # the reference's load_vad_model downloads (vad.py:28-43): a recording stand-in for it
+    ref_vad_calls = []
+    def ref_load_vad_model(device, vad_onset=0.5, vad_offset=0.363, use_auth_token=None, model_fp=None):
+        ref_vad_calls.append(model_fp)
+        return "reference-pyannote-pipeline"
+    whisperx.vad.load_vad_model = ref_load_vad_model
+    whisperx.asr.load_vad_model = ref_load_vad_model
+
     import whisperx_amd
     from whisperx_amd import vad as amd_vad, writers as amd_writers
     rebound = whisperx_amd.install(whisperx)
@@ -72,6 +80,31 @@ SCRIPT = textwrap.dedent(r'''
     assert whisperx.transcribe.cli.__globals__["align"] is whisperx_amd.align
     assert whisperx.transcribe.cli.__globals__["load_align_model"] is whisperx_amd.load_align_model
     assert whisperx.asr.FasterWhisperPipeline.transcribe.__globals__["merge_chunks"] is amd_vad.merge_chunks
+
+    # load_vad_model (asr.py:13, called by load_model at asr.py:347) is the drop-in producer,
+    # falling back to the reference's loader for what it cannot read
+    lv = whisperx.asr.load_model.__globals__["load_vad_model"]
+    assert lv is whisperx.asr.load_vad_model and lv._wx_reference is ref_load_vad_model
+    assert whisperx.vad.load_vad_model._wx_reference is ref_load_vad_model
+    whisperx_amd.install(whisperx)  # a second install must not wrap the drop-in again
+    assert whisperx.asr.load_vad_model._wx_reference is ref_load_vad_model
+    import hashlib, os, tempfile
+    from whisperx_amd import vad_model as amd_vm
+    tmp = tempfile.mkdtemp()
+    assert lv("cpu", model_fp=os.path.join(tmp, "absent.bin")) == "reference-pyannote-pipeline"
+    pickled = os.path.join(tmp, "lightning.bin")          # pickles a non-tensor object
+    torch.save({"state_dict": amd_vm.PyanNet().state_dict(), "loops": SimpleNamespace(epoch=3)}, pickled)
+    plain = os.path.join(tmp, "plain.bin")
+    torch.save(amd_vm.PyanNet().state_dict(), plain)
+    for fp, want_ref in ((pickled, True), (plain, False)):
+        digest = hashlib.sha256(open(fp, "rb").read()).hexdigest()   # as if it were the whisperX file
+        amd_vm.VAD_SEGMENTATION_URL = "https://x/segmentation/" + digest + "/pytorch_model.bin"
+        got = lv("cpu", vad_onset=0.45, model_fp=fp)
+        if want_ref:
+            assert got == "reference-pyannote-pipeline", got
+        else:
+            assert isinstance(got, amd_vm.VoiceActivitySegmentation) and got.hyperparameters["onset"] == 0.45
+    assert ref_vad_calls == [os.path.join(tmp, "absent.bin"), pickled], ref_vad_calls
     print("rebound", len(rebound))
 ''')
 

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import threading
 from typing import Optional
 
 import numpy as np
@@ -82,6 +83,7 @@ SIGNATURES = {
     "wx_binarize_workspace_bytes": (_sz, [_i32, _i64]),
     "wx_binarize_ex": (ctypes.c_int, [_vp, _vp, _i32, _i64, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                       _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "wx_binarize_plan": (ctypes.c_int, [_f32, _f32, _i64, ctypes.c_char_p, _sz]),
 }
 
 
@@ -163,18 +165,26 @@ def _dev_i64(x, device):
 
 
 class Workspace:
-    """Grow-only device scratch buffer (avoids an allocation per call)."""
+    """Grow-only device scratch buffers, one per (device, stream): calls enqueued on different
+    streams (or from different threads) never share scratch, as the ABI's reentrancy allows.
+    A buffer is allocated while its stream is current, so the caching allocator orders its
+    reuse after that stream's pending kernels when it is replaced by a larger one."""
 
     def __init__(self):
         self.buf: dict = {}
+        self._mu = threading.Lock()
 
-    def get(self, device, nbytes: int) -> torch.Tensor:
-        key = str(device)
-        b = self.buf.get(key)
-        if b is None or b.numel() < nbytes:
-            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-            self.buf[key] = b
-        return b
+    def get(self, device, nbytes: int, stream=None) -> torch.Tensor:
+        device = torch.device(device)
+        st = stream if stream is not None else torch.cuda.current_stream(device)
+        key = (str(device), int(st.cuda_stream))
+        with self._mu:
+            b = self.buf.get(key)
+            if b is None or b.numel() < nbytes:
+                with torch.cuda.device(device), torch.cuda.stream(st):
+                    b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+                self.buf[key] = b
+            return b
 
 
 _ws = Workspace()
@@ -191,13 +201,15 @@ class Handoff:
 
     def get(self, device, stream_handle: int, nbytes: int) -> torch.Tensor:
         key = (str(device), int(stream_handle))
-        b = self.buf.get(key)
-        if b is None or b.numel() < nbytes:
-            b = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
-            self.buf[key] = b
-        return b
+        with _handoff_mu:
+            b = self.buf.get(key)
+            if b is None or b.numel() < nbytes:
+                b = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=device)
+                self.buf[key] = b
+            return b
 
 
+_handoff_mu = threading.Lock()
 _handoff = Handoff()
 
 
@@ -295,10 +307,10 @@ def align_dp(b: Batch, mode: int = MODE_AUTO):
     t_start = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
     status = torch.empty(max(b.S, 1), dtype=torch.int32, device=dev)
     wsb = lib.wx_align_dp_workspace_bytes(b.S, b.sum_T, b.max_N)
-    ws = _ws.get(dev, wsb)
     hob = lib.wx_align_dp_handoff_bytes(b.S, b.sum_T)
     with torch.cuda.device(dev):
         stream = torch.cuda.current_stream(dev)
+        ws = _ws.get(dev, wsb, stream)  # per (device, stream): concurrent calls never share it
         ho = _handoff.get(dev, stream.cuda_stream, hob)
         _check(lib.wx_align_dp_ex(_ptr(b.em), _ptr(b.em_off_d), b.V, _ptr(b.tok), _ptr(b.tok_off_d),
                                   _ptr(b.blank), b.S, b.min_N, b.max_N, b.sum_T, _ptr(seg_start), _ptr(seg_end),
@@ -455,6 +467,15 @@ def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration
         a = r_off[i]
         out.append((rs[a:a + n].cpu().numpy(), re[a:a + n].cpu().numpy()))
     return out
+
+
+def binarize_plan(onset: float, offset: float, total_frames: int = 1):
+    """Kernel names (rocprof form) wx_binarize_ex launches for these thresholds."""
+    import numpy as np
+    lib = load(require_device=False)
+    buf = ctypes.create_string_buffer(512)
+    lib.wx_binarize_plan(float(np.float32(onset)), float(np.float32(offset)), int(total_frames), buf, len(buf))
+    return [x for x in buf.value.decode().split(";") if x]
 
 
 def vad_aggregate(scores: torch.Tensor, start_frames, n_frames: int, missing: float = float("nan")):

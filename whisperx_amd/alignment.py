@@ -25,6 +25,7 @@ There is no CPU fallback: without a HIP device the DP raises.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import time
@@ -442,22 +443,26 @@ def align(
         toks.append(tokens)
         blanks.append(blank_id)
         meta.append((text_clean, waveform_segment.size(0)))
-    with _Phase("emission"):
-        ems = _emissions(model, model_type, ems, device)
+    # the model is prepared (GEMM convolutions, wx attention) for this call only: the caller's
+    # model is restored when align() returns, after every forward has been joined
+    gpu_route = torch.device(device).type == "cuda" and not os.environ.get("WX_MIOPEN_CONV")
+    with emission.prepared(model) if gpu_route else contextlib.nullcontext():
+        with _Phase("emission"):
+            ems = _emissions(model, model_type, ems, device)
 
-    # 2b. the fused DP, one launch per group of segments, and 2c. timestamps and aggregation in
-    # segment order (same prints, same order).  A group's DP waits only for its own forwards, so
-    # the host aggregates group g while the GPU still runs the forwards of the later groups.
-    with _Phase("dp+aggregate"):
-        results = _GroupedDP(ems, toks, blanks, dp_dev)
-        try:
-            aligned_segments = _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method,
-                                              return_char_alignments)
-        finally:
-            if isinstance(ems, _EmissionsCSR):
-                main = torch.cuda.current_stream(dp_dev)
-                for st in ems.streams:
-                    main.wait_stream(st)
+        # 2b. the fused DP, one launch per group of segments, and 2c. timestamps and aggregation
+        # in segment order (same prints, same order).  A group's DP waits only for its own
+        # forwards, so the host aggregates group g while the GPU still runs the later forwards.
+        with _Phase("dp+aggregate"):
+            results = _GroupedDP(ems, toks, blanks, dp_dev)
+            try:
+                aligned_segments = _aggregate_all(transcript, plan, results, meta, model_lang, interpolate_method,
+                                                  return_char_alignments)
+            finally:
+                if isinstance(ems, _EmissionsCSR):
+                    main = torch.cuda.current_stream(dp_dev)
+                    for st in ems.streams:
+                        main.wait_stream(st)
     word_segments: List[SingleWordSegment] = []
     for segment in aligned_segments:
         word_segments += segment["words"]

@@ -3860,6 +3860,9 @@ int wx_binarize(const float* scores, const int64_t* f_off, int32_t n_files, cons
     return launch_status();
 }
 
+// offset <= onset: no frame both sets and resets the state, so the parallel scan is exact
+static bool binarize_uses_scan(float onset, float offset) { return offset <= onset; }
+
 size_t wx_binarize_workspace_bytes(int32_t n_files, int64_t total_frames) {
     if (n_files < 0 || total_frames < 0) return 0;
     const size_t nw = (size_t)bin_words(total_frames, n_files);
@@ -3903,7 +3906,7 @@ int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, i
     a.y = scores; a.f_off = f_off; a.sw_start = sw_start; a.sw_step = sw_step; a.sw_dur = sw_duration;
     a.onset = onset; a.offset = offset; a.maxd = max_duration; a.pad_on = pad_onset; a.pad_off = pad_offset;
     a.rs = reg_start; a.re = reg_end; a.reg_off = reg_off; a.reg_count = reg_count;
-    if (offset <= onset) {  // no frame both sets and resets: the parallel scan
+    if (binarize_uses_scan(onset, offset)) {
         BinScanArgs sa;
         sa.a = a; sa.w = w; sa.ra = ra; sa.rd = rd;
         hipLaunchKernelGGL(binarize_scan_kernel, dim3(n_files), dim3(kBinWG), 0, s, sa);
@@ -3911,6 +3914,23 @@ int wx_binarize_ex(const float* scores, const int64_t* f_off, int32_t n_files, i
         hipLaunchKernelGGL(binarize_fsm_kernel, dim3(n_files), dim3(kWave), 0, s, a, w);
     }
     return launch_status();
+}
+
+int wx_binarize_plan(float onset, float offset, int64_t total_frames, char* buf, size_t n) {
+    const char* words = "void wx::binarize_words_kernel(wx::BinWordArgs)";
+    const char* second = binarize_uses_scan(onset, offset) ? "void wx::binarize_scan_kernel(wx::BinScanArgs)"
+                                                           : "void wx::binarize_fsm_kernel(wx::BinarizeArgs, wx::BinWords)";
+    char all[256];
+    const int cnt = total_frames > 0 ? 2 : 1;
+    if (total_frames > 0)
+        snprintf(all, sizeof all, "%s;%s", words, second);
+    else
+        snprintf(all, sizeof all, "%s", second);
+    if (buf && n > 0) {
+        strncpy(buf, all, n - 1);
+        buf[n - 1] = 0;
+    }
+    return cnt;
 }
 
 }  // extern "C"

@@ -8,12 +8,18 @@ its own files with no collective on the data path.  The only collectives:
     (a few hundred bytes; backend "nccl" = RCCL over xGMI on ROCm, "gloo" on CPU);
   * gather_results (optional): per-file result dicts to rank 0 (gather_object).
 
+pin_rank splits the host CPUs between the ranks of a node (host CPU per rank —
+Python orchestration and the aggregation — is the scaling limiter): each local rank gets a
+disjoint slice of the process's CPU affinity and an intra-op thread pool of its share of the
+thread budget, so 8 ranks do not each start a pool over every core.
+
 shard_files balances mixed-length corpora (BASELINE config 4: 40 files of 1-60 min)
 longest-processing-time first: files sorted by duration (descending, index as tie
 break), each assigned to the currently least-loaded rank (lowest rank on ties).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -34,6 +40,49 @@ def shard_files(durations: Sequence[float], world_size: int) -> List[List[int]]:
     for s in shards:
         s.sort()
     return shards
+
+
+def thread_budget() -> int:
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS (a
+    shared box's os.cpu_count() counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(n, 1)
+
+
+def rank_cpus(cpus: Sequence[int], local_rank: int, local_world: int) -> List[int]:
+    """Local rank's share of `cpus`: contiguous slices of the sorted list, disjoint across the
+    ranks and together covering it (more ranks than CPUs: one CPU each, round robin)."""
+    if local_world < 1 or not 0 <= local_rank < local_world:
+        raise ValueError(f"local rank {local_rank} outside a node of {local_world}")
+    cpus = sorted(int(c) for c in cpus)
+    n = len(cpus)
+    if n == 0:
+        return []
+    if local_world > n:
+        return [cpus[local_rank % n]]
+    return cpus[local_rank * n // local_world:(local_rank + 1) * n // local_world]
+
+
+def pin_rank(local_rank: Optional[int] = None, local_world: Optional[int] = None) -> dict:
+    """Pin this rank to its disjoint CPU slice and size torch's intra-op pool to its share of
+    the thread budget.  Call before any GPU work (HIP's runtime threads inherit the affinity).
+    Defaults: LOCAL_RANK / LOCAL_WORLD_SIZE from torchrun.  Returns {"cpus", "threads"}."""
+    lr = int(os.environ.get("LOCAL_RANK", "0")) if local_rank is None else int(local_rank)
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if local_world is None else int(local_world)
+    budget = thread_budget()
+    if not hasattr(os, "sched_getaffinity"):
+        threads = max(1, budget // max(lw, 1))
+        torch.set_num_threads(threads)
+        return {"cpus": None, "threads": threads}
+    mine = rank_cpus(os.sched_getaffinity(0), lr, lw)
+    if mine:
+        os.sched_setaffinity(0, mine)
+    threads = max(1, min(len(mine) or 1, budget // max(lw, 1)))
+    torch.set_num_threads(threads)
+    return {"cpus": mine, "threads": threads}
 
 
 def _encode_dictionary(d: Dict[str, int]) -> torch.Tensor:

@@ -36,7 +36,9 @@ PyTorch-ROCm model call, one per segment, but:
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 import types
 from typing import List, Optional, Sequence
 
@@ -172,17 +174,34 @@ def _wx_attention(module, query, key, value, attention_mask, dropout: float = 0.
     wx_attention_f32 (f32 MFMA flash attention); anything else (masks, dropout, other dtypes
     or head sizes, attention weights requested) through transformers' SDPA interface."""
     if (query.is_cuda and attention_mask is None and not (dropout and module.training) and not torch.is_grad_enabled()
-            and not kwargs.get("output_attentions") and query.dtype == torch.float32 and query.shape[-1] == 64
+            and not any(v is not None and v is not False for v in kwargs.values())
+            and query.dtype == torch.float32 and query.shape[-1] == 64
             and key.shape == query.shape and value.shape == query.shape and query.stride(-1) == 1
             and key.stride(-1) == 1 and value.stride(-1) == 1):
         from . import _lib
 
         scale = scaling if scaling is not None else query.shape[-1] ** -0.5
         return _lib.attention_f32(query, key, value, scale), None
+    return _orig_attention(module)(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
+                                   **kwargs)
+
+
+# config id -> the attention implementation prepare_model replaced (its fallback target)
+_ORIG_ATTN: dict = {}
+
+
+def _orig_attention(module):
+    """The attention function the model used before prepare_model: the interface registered
+    under its original `_attn_implementation`, or the modeling file's eager attention."""
+    import sys
+
     from transformers.modeling_utils import ALL_ATTENTION_FUNCTIONS
 
-    return ALL_ATTENTION_FUNCTIONS["sdpa"](module, query, key, value, attention_mask, dropout=dropout,
-                                           scaling=scaling, **kwargs)
+    eager = getattr(sys.modules.get(type(module).__module__), "eager_attention_forward", None)
+    name = _ORIG_ATTN.get(id(getattr(module, "config", None)), "sdpa")
+    if name and name != "eager" and name in ALL_ATTENTION_FUNCTIONS:
+        return ALL_ATTENTION_FUNCTIONS[name]
+    return eager if eager is not None else ALL_ATTENTION_FUNCTIONS["sdpa"]
 
 
 def _use_wx_attention(model: torch.nn.Module) -> None:
@@ -199,6 +218,7 @@ def _use_wx_attention(model: torch.nn.Module) -> None:
         orig = cfg._attn_implementation
         cfg._attn_implementation = _ATTN_NAME
         model._wx_orig_attn = orig
+        _ORIG_ATTN[id(cfg)] = orig
     except Exception:  # an older transformers without the interface: torch's attention stays
         pass
 
@@ -227,17 +247,51 @@ def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
 
 
 def restore_model(model: torch.nn.Module) -> torch.nn.Module:
-    """Undo prepare_model."""
+    """Undo prepare_model: the original forwards, attention implementation and no cached
+    weights (the model is then exactly what the caller passed in)."""
     for mod in model.modules():
         if hasattr(mod, "_wx_orig_forward"):
-            mod.forward = mod._wx_orig_forward
+            orig = mod._wx_orig_forward
+            if getattr(orig, "__func__", None) is getattr(type(mod), "forward", None):
+                mod.__dict__.pop("forward", None)  # the class's forward again, no instance attribute
+            else:
+                mod.forward = orig  # the module had its own instance-level forward
             del mod._wx_orig_forward
-    if getattr(model, "_wx_gemm_conv", False):
-        model._wx_gemm_conv = False
+        if hasattr(mod, "_wx_w_cache"):
+            del mod._wx_w_cache
+    if "_wx_gemm_conv" in model.__dict__:
+        del model._wx_gemm_conv
     if hasattr(model, "_wx_orig_attn"):
+        _ORIG_ATTN.pop(id(model.config), None)
         model.config._attn_implementation = model._wx_orig_attn
         del model._wx_orig_attn
     return model
+
+
+_PREP_MU = threading.Lock()
+
+
+@contextlib.contextmanager
+def prepared(model: torch.nn.Module):
+    """prepare_model for the duration of one align() call (reference alignment.py:226-233
+    takes the caller's model and leaves it as it was).  Concurrent calls on one model share
+    the preparation; the last one to leave restores the model, unless the caller had
+    prepared it already."""
+    with _PREP_MU:
+        refs = model.__dict__.get("_wx_prep_refs", 0)
+        if refs == 0:
+            model.__dict__["_wx_prep_owned"] = not getattr(model, "_wx_gemm_conv", False)
+            prepare_model(model)
+        model.__dict__["_wx_prep_refs"] = refs + 1
+    try:
+        yield model
+    finally:
+        with _PREP_MU:
+            model.__dict__["_wx_prep_refs"] -= 1
+            if model.__dict__["_wx_prep_refs"] == 0:
+                if model.__dict__.pop("_wx_prep_owned", False):
+                    restore_model(model)
+                del model.__dict__["_wx_prep_refs"]
 
 
 def batchable(model) -> bool:

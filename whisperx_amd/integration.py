@@ -5,7 +5,7 @@ The reference binds the alignment/VAD names at import time in several modules, s
 
   whisperx/__init__.py:2    from .alignment import load_align_model, align
   whisperx/transcribe.py:9  from .alignment import align, load_align_model   (CLI, :188,:201,:203)
-  whisperx/asr.py:13        from .vad import load_vad_model, merge_chunks      (:187)
+  whisperx/asr.py:13        from .vad import load_vad_model, merge_chunks      (:187, :347)
   whisperx/transcribe.py:13 from .utils import ... get_writer ...
 
 ``install()`` rebinds every one of those names, in every module of the package that holds
@@ -22,6 +22,29 @@ import sys
 from typing import Dict, List, Optional, Tuple
 
 
+def _vad_loader(reference_loader):
+    """The drop-in for the reference's load_vad_model (vad.py:20-59, bound at asr.py:13 and
+    called at asr.py:347): this package's producer (PyanNet + wx_vad_aggregate, scores kept on
+    the device) when the checkpoint loads without executing anything from it; otherwise —
+    a pickled Lightning checkpoint, another key layout, or no local file (the reference then
+    downloads it) — the reference's own pyannote pipeline, with a one-line notice."""
+    from . import vad_model
+
+    def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=None, model_fp=None):
+        try:
+            return vad_model.load_vad_model(device, vad_onset=vad_onset, vad_offset=vad_offset,
+                                            use_auth_token=use_auth_token, model_fp=model_fp)
+        except (vad_model.CheckpointNotLoadable, FileNotFoundError) as e:
+            print(f"whisperx_amd: VAD producer not used ({str(e).splitlines()[0][:160]}); "
+                  f"falling back to the reference's pyannote pipeline")
+            return reference_loader(device, vad_onset=vad_onset, vad_offset=vad_offset,
+                                    use_auth_token=use_auth_token, model_fp=model_fp)
+
+    load_vad_model._wx_reference = reference_loader
+    load_vad_model.__doc__ = _vad_loader.__doc__
+    return load_vad_model
+
+
 def _targets() -> Dict[str, Dict[str, object]]:
     from . import alignment, vad, writers
 
@@ -33,8 +56,8 @@ def _targets() -> Dict[str, Dict[str, object]]:
         "alignment": align_names,
         "transcribe": {"align": alignment.align, "load_align_model": alignment.load_align_model,
                        "get_writer": writers.get_writer},
-        "asr": {"merge_chunks": vad.merge_chunks},
-        "vad": {"merge_chunks": vad.merge_chunks, "Binarize": vad.Binarize},
+        "asr": {"merge_chunks": vad.merge_chunks, "load_vad_model": _vad_loader},
+        "vad": {"merge_chunks": vad.merge_chunks, "Binarize": vad.Binarize, "load_vad_model": _vad_loader},
         "utils": {"get_writer": writers.get_writer},
     }
 
@@ -61,6 +84,11 @@ def install(whisperx=None, import_missing: bool = True) -> List[Tuple[str, str]]
             continue
         for name, obj in names.items():
             if hasattr(mod, name):
+                if obj is _vad_loader:  # wraps the module's own loader (its fallback)
+                    cur = getattr(mod, name)
+                    if hasattr(cur, "_wx_reference"):
+                        continue  # installed already
+                    obj = _vad_loader(cur)
                 setattr(mod, name, obj)
                 done.append((modname, name))
     return done
@@ -78,6 +106,9 @@ def installed(whisperx=None) -> Optional[bool]:
         if mod is None:
             continue
         for name, obj in names.items():
-            if hasattr(mod, name) and getattr(mod, name) is not obj:
+            if not hasattr(mod, name):
+                continue
+            cur = getattr(mod, name)
+            if (obj is _vad_loader and not hasattr(cur, "_wx_reference")) or (obj is not _vad_loader and cur is not obj):
                 return False
     return True

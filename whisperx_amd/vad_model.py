@@ -336,6 +336,12 @@ class VoiceActivitySegmentation:
         return self
 
 
+class CheckpointNotLoadable(RuntimeError):
+    """The segmentation checkpoint cannot be read without executing code from it (a pickled
+    Lightning checkpoint) or is not a PyanNet state_dict.  whisperx_amd.install()'s drop-in
+    load_vad_model then falls back to the reference's own pyannote pipeline."""
+
+
 VAD_SEGMENTATION_URL = ("https://whisperx.s3.eu-west-2.amazonaws.com/model_weights/segmentation/"
                         "0b5b3216d60a2d32fc086b47ea8c67589aaeb26b7e07fcbe620d6d0b83e209ea/pytorch_model.bin")
 
@@ -348,7 +354,13 @@ def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=Non
     (`check_sha256=False` for a checkpoint of one's own), read with
     ``torch.load(..., weights_only=True)`` (nothing in the file is executed) and loaded into a
     PyanNet; returns the producer pipeline with the reference's hyper-parameters.  A file that
-    is absent raises (offline: there is nothing to fetch it from)."""
+    is absent raises FileNotFoundError (offline: there is nothing to fetch it from); one that
+    torch.load(weights_only=True) refuses, or whose keys are not PyanNet's, raises
+    CheckpointNotLoadable.  Loading the real whisperX checkpoint (a pyannote/Lightning file)
+    is untested here — pyannote and the file are absent — so its parity is unpinned: the
+    expected layout is pyannote 3.1's PyanNet state_dict (sincnet.wav_norm1d,
+    sincnet.conv1d.{0,1,2}, sincnet.norm1d.{0,1,2}, lstm.weight_ih_l{k}[_reverse] ...,
+    linear.{0,1}, classifier), as ``PyanNet().state_dict()`` lists it."""
     if model_fp is None:
         model_fp = os.path.join(torch.hub._get_torch_home(), "whisperx-vad-segmentation.bin")
     if os.path.exists(model_fp) and not os.path.isfile(model_fp):
@@ -365,9 +377,14 @@ def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=Non
     try:
         ckpt = torch.load(model_fp, map_location="cpu", weights_only=True)
     except Exception as e:  # a Lightning checkpoint with pickled non-tensor objects
-        raise RuntimeError(f"{model_fp}: torch.load(weights_only=True) refused the file ({e}); save its "
-                           f"'state_dict' entry on its own and pass that file") from e
-    model = PyanNet.from_pyannote_state_dict(ckpt)
+        raise CheckpointNotLoadable(
+            f"{model_fp}: torch.load(weights_only=True) refused the file ({str(e).splitlines()[0][:200]}); "
+            f"this loader executes nothing from a checkpoint: export its 'state_dict' entry (tensors "
+            f"only, pyannote's key names) with tooling you trust and pass that file") from e
+    try:
+        model = PyanNet.from_pyannote_state_dict(ckpt)
+    except (KeyError, RuntimeError, AttributeError) as e:
+        raise CheckpointNotLoadable(f"{model_fp}: not a PyanNet segmentation state_dict ({e})") from e
     pipeline = VoiceActivitySegmentation(segmentation=model, device=torch.device(device))
     return pipeline.instantiate({"onset": vad_onset, "offset": vad_offset, "min_duration_on": 0.1,
                                  "min_duration_off": 0.1})
