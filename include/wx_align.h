@@ -226,15 +226,6 @@ int wx_attention_f32(const float* q, const float* k, const float* v, float* o, i
                      int32_t D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                      float scale, void* stream);
 
-/* wx_attention_f32 over a ragged batch of segments (the batched emission forward): segment s
- * is rows [row_off[s], row_off[s+1]) of [sum_T, H, 64] q/k/v (element strides {row, head}, head
- * dim contiguous) and of o ([sum_T, H, 64] contiguous); it attends within itself only.
- * tile_off[s] = sum over s' < s of ceil(T_s' / 32), n_tiles = tile_off[S]; row_off and
- * tile_off are device arrays. */
-int wx_attention_f32_csr(const float* q, const float* k, const float* v, float* o, int32_t S, int32_t H, int32_t D,
-                         const int64_t* row_off, const int32_t* tile_off, int32_t n_tiles, const int64_t* q_strides,
-                         const int64_t* k_strides, const int64_t* v_strides, float scale, void* stream);
-
 /* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
  * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32
  * (the segmentation model's sigmoid outputs per chunk), start_frame[c] = the file-grid frame

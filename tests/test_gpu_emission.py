@@ -54,54 +54,6 @@ def test_attention_f32_vs_fp64(B, H, T):
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
 
 
-def test_attention_f32_csr_vs_fp64():
-    """wx_attention_f32_csr on a ragged batch (segments of 1, 31, 33, 400 and 1,499 rows,
-    including an empty one) against an fp64 attention within each segment."""
-    from whisperx_amd import _lib
-
-    torch.manual_seed(1)
-    Ts = [31, 1, 0, 400, 33, 1499]
-    R, H = sum(Ts), 12
-    proj = [torch.randn(R, H * 64, device="cuda") * 2 for _ in range(3)]
-    q, k, v = (p.view(R, H, 64) for p in proj)
-    got = _lib.attention_f32_csr(q, k, v, Ts, 0.125)
-    o = 0
-    for t in Ts:
-        qd, kd, vd = (x[o:o + t].transpose(0, 1).double() for x in (q, k, v))
-        ref = (torch.softmax(qd @ kd.transpose(-1, -2) * 0.125, -1) @ vd).transpose(0, 1).float()
-        torch.testing.assert_close(got[o:o + t], ref, rtol=1e-5, atol=2e-5)
-        o += t
-
-
-@pytest.mark.parametrize("stable", [False, True])
-def test_batched_logits_vs_per_segment_forward_gpu(stable):
-    """The batched emission forward (emission.batched_logits: concatenated rows, ragged
-    attention) against each segment's own prepared forward on the GPU: log-probabilities within
-    float noise, identical frame argmax."""
-    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
-
-    from whisperx_amd import emission
-
-    torch.manual_seed(2)
-    if stable:
-        cfg = Wav2Vec2Config(vocab_size=40, num_hidden_layers=4, hidden_size=1024, num_attention_heads=16,
-                             intermediate_size=4096, feat_extract_norm="layer", do_stable_layer_norm=True, conv_bias=True)
-    else:
-        cfg = Wav2Vec2Config(vocab_size=32)
-    m = Wav2Vec2ForCTC(cfg).cuda().eval()
-    emission.prepare_model(m)
-    rng = np.random.default_rng(3)
-    wavs = [torch.from_numpy(rng.standard_normal(n).astype(np.float32) * 0.1).cuda() for n in (480000, 400, 117000, 33333)]
-    got = emission.batched_logits(m, wavs)
-    for w, g in zip(wavs, got):
-        with torch.inference_mode():
-            ref = m(w.reshape(1, -1)).logits[0]
-        assert g.shape == ref.shape
-        lg, lr = torch.log_softmax(g, -1), torch.log_softmax(ref, -1)
-        assert (lg - lr).abs().max().item() <= 5e-5
-        assert torch.equal(lg.argmax(-1), lr.argmax(-1))
-
-
 def _check_prepared_vs_stock(m, V, lengths, tol=5e-5):
     from whisperx_amd import emission
 
@@ -156,23 +108,16 @@ def test_prepared_large_xlsr_forward_matches_stock():
     print(f"large-xlsr prepared vs stock: max |dlogp| = {worst:.3g}")
 
 
-@pytest.mark.parametrize("batched", [False, True])
-def test_emissions_fan_out_fresh_parametrised_model(monkeypatch, batched):
+def test_emissions_fan_out_fresh_parametrised_model():
     """the positional conv's weight_norm weight is cached; on a freshly
     built model the cache must exist before the forwards fan out over 8 streams, or the
     streams read it before it is computed.  Segment 0 is much longer than the others (its
     stream would still be building the weight when the others reach the positional conv).
-    Every segment's emission must equal a single-stream forward of the same model (per-segment
-    forwards: to 1e-6; batched forwards, whose GEMMs have other row counts: to float noise with
-    identical frame argmax)."""
+    Every segment's emission must equal a single-stream forward of the same model to 1e-6."""
     from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
 
     from whisperx_amd import alignment, emission
 
-    if batched:
-        monkeypatch.setenv("WX_EMISSION_BATCH", "8")
-    else:
-        monkeypatch.delenv("WX_EMISSION_BATCH", raising=False)
     torch.manual_seed(2)
     m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
     pos = m.wav2vec2.encoder.pos_conv_embed.conv
@@ -189,7 +134,7 @@ def test_emissions_fan_out_fresh_parametrised_model(monkeypatch, batched):
         for i, w in enumerate(wavs):
             ref = torch.log_softmax(m(w).logits, -1)[0]
             err = float((csr[i] - ref).abs().max())
-            assert err <= (5e-5 if batched else 1e-6), f"segment {i}: fan-out emission differs from single-stream by {err}"
+            assert err <= 1e-6, f"segment {i}: fan-out emission differs from single-stream by {err}"
             assert torch.equal(csr[i].argmax(-1), ref.argmax(-1))
     emission.restore_model(m)
 

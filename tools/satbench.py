@@ -138,6 +138,20 @@ def child(args):
                                            "merge": float(np.median(mrg)), "per_step_fwd": float(np.median(fwd)) / T,
                                            "per_step_walk": float(np.median(walk)) / T,
                                            "walk_max": float(walk.max()), "fwd_max": float(fwd.max())}
+            if args.parts > 1 and hasattr(lib, "wx_debug_cq"):
+                cbuf = (ctypes.c_ulonglong * (n * 48 * 3))()
+                lib.wx_debug_cq(cbuf, n)
+                cq = np.frombuffer(cbuf, dtype=np.uint64).reshape(n, 48, 3).astype(np.int64)[perm]
+                cq = cq.reshape(-1, args.parts, 48, 3)
+                t0 = cq[:, 0, 0, 0][:, None, None]
+                rel = (cq - t0[..., None]) / 100.0  # us since part 0 passed barrier 0
+                nq = (T + 31) // 32
+                out[case]["chunk_start_us_by_part_med"] = [[round(float(np.median(rel[:, p_, q, 0])), 2) for q in range(0, nq, 4)]
+                                                           for p_ in range(args.parts)]
+                out[case]["granule_store_us_by_part_med"] = [[round(float(np.median(rel[:, p_, q, 1])), 2) for q in range(1, nq, 4)]
+                                                             for p_ in range(args.parts)]
+                out[case]["granule_seen_us_by_part_med"] = [[round(float(np.median(rel[:, p_, q, 2])), 2) for q in range(1, nq, 4)]
+                                                            for p_ in range(args.parts)]
             lbuf = (ctypes.c_ulonglong * (n * 16 * 3))()
             lib.wx_debug_loop(lbuf, n)
             lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)[perm]
@@ -202,7 +216,8 @@ def main():
             print(f"  {case:9s} {v['ms_med']:9.4f} ms  {v['cells_per_s']:.3e} cells/s  frac {v['frac']:.3f}", flush=True)
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
-                for k in ("fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
+                for k in ("chunk_start_us_by_part_med", "granule_store_us_by_part_med", "granule_seen_us_by_part_med",
+                          "fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
                           "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_rl_med(cycles,changes,blocks)", "walk_split_med(argmax,walk,compact)",
                           "handoff_med(misses,wait_cyc,slack_cyc)"):
                     if k in v:

@@ -76,8 +76,6 @@ SIGNATURES = {
     "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
-    "wx_attention_f32_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp,
-                                            _f32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
     "wx_binarize_workspace_bytes": (_sz, [_i32, _i64]),
@@ -521,29 +519,6 @@ def attention_f32(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: floa
     with torch.cuda.device(q.device):
         _check(lib.wx_attention_f32(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, T, D, st[0], st[1], st[2],
                                     float(scale), _stream(q.device)))
-    return o
-
-
-def attention_f32_csr(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, Ts, scale: float) -> torch.Tensor:
-    """wx_attention_f32_csr: per-segment softmax(scale * q k^T) v over a ragged batch.  q/k/v:
-    [sum_T, H, 64] fp32 device views (head dim contiguous); Ts: the segments' row counts.
-    Returns [sum_T, H, 64]."""
-    lib = load()
-    R, H, D = (int(x) for x in q.shape)
-    Ts = [int(t) for t in Ts]
-    if sum(Ts) != R or tuple(k.shape) != (R, H, D) or tuple(v.shape) != (R, H, D):
-        raise WXError(f"attention_f32_csr: shapes {tuple(q.shape)}, {tuple(k.shape)}, {tuple(v.shape)} vs rows {sum(Ts)}")
-    rows = np.zeros(len(Ts) + 1, np.int64)
-    rows[1:] = np.cumsum(Ts)
-    tiles = np.zeros(len(Ts) + 1, np.int32)
-    tiles[1:] = np.cumsum([(t + 31) // 32 for t in Ts])
-    offs = torch.from_numpy(np.concatenate([rows, tiles.astype(np.int64)])).to(q.device, non_blocking=False)
-    row_d, tile_d = offs[: len(Ts) + 1], offs[len(Ts) + 1:].to(torch.int32)
-    o = torch.empty((R, H, D), dtype=torch.float32, device=q.device)
-    st = [(ctypes.c_int64 * 2)(*(int(x) for x in t.stride()[:2])) for t in (q, k, v)]
-    with torch.cuda.device(q.device):
-        _check(lib.wx_attention_f32_csr(_ptr(q), _ptr(k), _ptr(v), _ptr(o), len(Ts), H, D, _ptr(row_d), _ptr(tile_d),
-                                        int(tiles[-1]), st[0], st[1], st[2], float(scale), _stream(q.device)))
     return o
 
 

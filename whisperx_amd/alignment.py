@@ -315,31 +315,6 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     csr.events = []
     for st in streams:
         st.wait_stream(main)
-    if model_type == "huggingface" and emission.batchable(model):
-        # batched forwards (emission.batched_logits): WX_EMISSION_BATCH segments per group, the
-        # groups round-robin on the streams; one event per group
-        G = max(1, int(os.environ.get("WX_EMISSION_BATCH", "8")))  # (batchable: > 0)
-        for g0 in range(0, len(waveforms), G):
-            st = streams[(g0 // G) % len(streams)]
-            with torch.cuda.stream(st):
-                ws = [w if w.shape[-1] >= 400 else torch.nn.functional.pad(w, (0, 400 - w.shape[-1]))
-                      for w in waveforms[g0:g0 + G]]  # alignment.py:217-221
-                lgs = emission.batched_logits(model, [w.to(dev) for w in ws])
-                if any(tuple(lg.shape) != (Ts[g0 + i], V) for i, lg in enumerate(lgs)):
-                    bad = True
-                    break
-                with torch.inference_mode():
-                    for i, lg in enumerate(lgs):
-                        emission.log_softmax_into(lg, csr[g0 + i])
-                ev = torch.cuda.Event()
-                ev.record(st)
-                csr.events.extend([ev] * len(lgs))
-        if bad:
-            for st in streams:
-                main.wait_stream(st)
-            return [_emission(model, model_type, w, device) for w in waveforms]
-        csr.streams = streams
-        return csr
     for i, w in enumerate(waveforms):
         st = streams[i % len(streams)]
         with torch.cuda.stream(st):

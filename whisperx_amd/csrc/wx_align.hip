@@ -51,15 +51,6 @@ namespace wx {
 constexpr int kWave = 64;
 constexpr int kChunk = 32;  // emission rows per LDS buffer == bits per column word
 constexpr int kUnroll = 8;  // time steps per unrolled group
-#ifndef WX_C8_UNROLL
-#define WX_C8_UNROLL 8  // ... for C >= 8 non-pipelined waves (Forward::kU; 4: A/B neutral)
-#endif
-#ifndef WX_COUNTED_WAIT
-#define WX_COUNTED_WAIT 0  // chunk-boundary wait skips the previous chunk's bitmap stores (A/B knob)
-#endif
-#ifndef WX_PIPE_C8W
-#define WX_PIPE_C8W 0  // A/B knob: software-pipelined operands in the multi-wave C = 8 buckets (no gain)
-#endif
 constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
 __device__ __forceinline__ float nan_max(float a, float b) {
@@ -71,17 +62,10 @@ __device__ __forceinline__ float nan_max(float a, float b) {
 // 32-step column word with an add-with-carry.
 __device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
     unsigned r;
-#ifdef WX_SHIFT_SGPR
-    unsigned long long m;
-    asm("v_cmp_gt_f32_e64 %1, %2, %3\n\tv_addc_co_u32_e64 %0, %1, %4, %4, %1"
-        : "=v"(r), "=&s"(m)
-        : "v"(c), "v"(s), "v"(w));
-#else
     asm("v_cmp_gt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %3, %3, vcc"
         : "=v"(r)
         : "v"(c), "v"(s), "v"(w)
         : "vcc");
-#endif
     return r;
 }
 
@@ -217,13 +201,8 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ E, int V, i
                 glds_dwordx4(E + (int64_t)(r0 + i * 8) * 32, (unsigned)l * 16u, base + (unsigned)(i * 1024));
         }
     } else if (l < V) {
-        for (int r = wv; r < nrows; r += W) {
-#ifdef WX_GLDS_BUILTIN
-            __builtin_amdgcn_global_load_lds(E + (int64_t)(r0 + r) * V + l, dst + r * VS, 4, 0, 0);
-#else
+        for (int r = wv; r < nrows; r += W)
             glds_dword(E + (int64_t)(r0 + r) * V, (unsigned)l * 4u, base + (unsigned)(r * VS * 4));
-#endif
-        }
     }
 }
 
@@ -291,12 +270,6 @@ __device__ int build_colmap(const int32_t* __restrict__ tok, int N, int blank, i
 }
 
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// all but the N most recent vector memory operations of this wave (they complete in order)
-template <int N>
-__device__ __forceinline__ void wait_vm_but() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 __device__ __forceinline__ void wave_fence() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -365,6 +338,11 @@ struct Layout {
 __device__ unsigned long long wx_phase[8192 * 6];
 // per (segment, wave): cycles in steps / barrier waits / other chunk work
 __device__ unsigned long long wx_loop[8192 * 16 * 3];
+// per (workgroup, chunk): s_memrealtime when wave 0 passed barrier q, when wave W-1 stored
+// chunk q's halo granules, when wave 0 had chunk q's halo (split kernels)
+__device__ unsigned long long wx_cq[8192 * 48 * 3];
+#define WX_CQ(q, i) \
+    if (lane_id() == 0 && blockIdx.x < 8192 && (q) < 48) wx_cq[(blockIdx.x * 48 + (q)) * 3 + (i)] = __builtin_amdgcn_s_memrealtime()
 #define WX_T(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define WX_STAMP(i) \
     if (threadIdx.x == 0 && blockIdx.x < 8192) wx_phase[blockIdx.x * 6 + (i)] = __builtin_amdgcn_s_memtime()
@@ -374,6 +352,7 @@ __device__ unsigned long long wx_loop[8192 * 16 * 3];
 #define WX_STAMP(i)
 #define WX_STAMP_RT(i)
 #define WX_T(v)
+#define WX_CQ(q, i)
 #endif
 
 // The trellis forward pass shared by the fused and the materialising kernels.
@@ -411,10 +390,7 @@ __host__ __device__ constexpr unsigned split_grid(int S, int P) {
 }
 constexpr int kHaloCells = 40;  // >= HL * C = ceil(32 / C) * C for every C
 constexpr int kMaxSpin = 1 << 16;
-#ifndef WX_XSLACK
-#define WX_XSLACK 1
-#endif
-constexpr int kXSlack = WX_XSLACK;  // chunks a part re-builds its lag to (A/B: 1 >= 2 > 3 > 4)
+constexpr int kXSlack = 1;  // chunks a part re-builds its lag to (A/B: 1 >= 2 > 3 > 4)
 
 struct Split {
     int p, P;         // this part, parts per segment
@@ -467,24 +443,19 @@ struct Forward {
     // Software-pipelined LDS operands where the extra registers keep the occupancy that
     // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
-    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && (W == 1 || WX_PIPE_C8W))));
+    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
     using Geo = Geometry<C, (SP ? 2 : W)>;  // SP: always a halo (the waves span P parts)
     // Steps per unrolled group of the non-pipelined chunk (hipcc hoists the group's LDS
     // loads; a multiple of 4: column-N history is stored as float4).
-    static constexpr int kU = C >= 8 ? WX_C8_UNROLL : kUnroll;
+    static constexpr int kU = kUnroll;
     static_assert(!(H && MODE == 1), "the materialising kernel computes column 0 in wave 0");
     // Register-resident chunks (split kernels with one cell per lane, the latency shape of
     // config 2): a chunk's operands are read into registers during the previous chunk (16-byte
     // reads of quad-interleaved rows), so the 32 steps of a chunk are a pure VALU chain — no
     // LDS read, no wait.  Micro-benchmarks (tools/ubench/step*.hip): a step costs ~20 cycles
     // of one wave alone, each LDS read issued inside the chain ~9 more.
-#ifndef WX_NO_REG_CHUNK
     static constexpr bool kReg = C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS;
-#else
-    static constexpr bool kReg = false;
-#endif
     static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
-    static constexpr bool kCountedWait = WX_COUNTED_WAIT && MODE == 0 && !SP;
     static constexpr int kQS = quad_stride<VS>();
 
     // Per-lane state of the forward pass.
@@ -676,18 +647,15 @@ struct Forward {
 #pragma unroll
                 for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
             }
+            if (SP && xpub) WX_CQ(q, 1);
             WX_T(c1);
             // this wave's staging (with a helper, DP waves stage nothing).  Single-CU fused
             // launches: not the previous chunk's C bitmap stores, issued last (the wait would
             // expose a store round trip per chunk)
-            if (!H) {
-                if (kCountedWait && q > 0)
-                    wait_vm_but<C>();
-                else
-                    wait_vm();
-            }
+            if (!H) wait_vm();
             __syncthreads();
             WX_T(c2);
+            if (wv == 0) WX_CQ(q, 0);
             if (W > 1 && q > 0 && halo && wv > 0) {
 #pragma unroll
                 for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
@@ -703,6 +671,7 @@ struct Forward {
                 // measured no better.)
                 WX_T(x0);
                 const bool missed = !xwait(sp->xin, sp->xstride, q, l, sp->tag, xpre, xlost, sp->spin);
+                WX_CQ(q, 2);
                 if (l < Geo::HL) {
 #pragma unroll
                     for (int k = 0; k < C; ++k) st.cur[k] = __builtin_bit_cast(float, (unsigned)xpre[k]);
@@ -742,6 +711,11 @@ struct Forward {
                 const char* nb = reinterpret_cast<const char*>(lds + ((q + 1 < nch ? q + 1 : q) % kBufs) * kBufFloats);
                 float cur0 = st.cur[0];
                 reg_chunk(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T);
+                // Invariant: on a partial last chunk reg_chunk runs all 32 steps on stale rows,
+                // so st.cur then holds the cell 32 steps on, not `rows` steps: nothing reads the
+                // state after the last chunk (its bits are masked below, column N stops at T).
+                // A change that publishes or reads the final cell state must keep
+                // hist[(rows - 1) & 7] instead.
                 st.cur[0] = cur0;
                 st.t += rows;
             } else if (vw == 0) {
@@ -921,7 +895,7 @@ struct Forward {
     // straight into the quad layout needs 16 instructions per chunk: measured ~1,600 cycles of
     // issue per chunk, more than a DP chunk; register staging one chunk ahead stalled on the
     // loads.)
-    static constexpr int kRing = 4;
+    static constexpr int kRing = 4;  // (A/B: 8 was 1.5 us slower on config 2)
     static constexpr int kPairs = 8 * VS / kWave;  // (row quad, column) pairs per lane
     __device__ __forceinline__ static void transpose_quads(const float* raw, float* buf) {
         const int l = lane_id();
@@ -946,9 +920,82 @@ struct Forward {
     // while they compute chunk q.  Quad buffer (q + 2) % kBufs (five) last held chunk q - 3,
     // whose operand reads the DP waves waited for before chunk q - 3's steps and whose column
     // 0 the helper read during chunk q - 5.
+    // The stager of a V == 32 batch with 16-byte aligned rows, through registers: lane l loads
+    // 16 bytes (columns 4 cg .. 4 cg + 3, cg = (l >> 2) & 7) of row 8 i + 4 h + j (j = l & 3,
+    // h = l >> 5) of a chunk with one global_load_dwordx4 per i (4 per chunk) and writes them
+    // into the quad layout with 16 ds_write_b32 (row quad 2 i + h, columns 4 cg + m, row j):
+    // no LDS-DMA ring and no LDS -> LDS transpose (which cost ~1,200 cycles per chunk and paced
+    // every part).  Four register sets: chunk c is loaded at iteration c - 6 (rows clamped into
+    // the segment, so the loads are unconditional and the compiler counts them exactly) and
+    // written before barrier c - 2, so each load has four chunk-times to land.
+    static constexpr int kStgSets = 4;
+    struct StgSet {
+        float4 v[4];
+    };
+    __device__ __forceinline__ static void stg_load(StgSet& s, const float* __restrict__ E, int T, int c) {
+        const int l = lane_id();
+        const int r = 4 * (l >> 5) + (l & 3), cg = (l >> 2) & 7;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = min(c * kChunk + 8 * i + r, T - 1);
+            s.v[i] = *reinterpret_cast<const float4*>(E + (int64_t)t * 32 + 4 * cg);
+        }
+    }
+    __device__ __forceinline__ static void stg_write(const StgSet& s, float* buf) {
+        const int l = lane_id();
+        const int cg = (l >> 2) & 7;
+        float* o = buf + (l >> 5) * kQS + 16 * cg + (l & 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i * kQS + 0] = s.v[i].x;
+            o[2 * i * kQS + 4] = s.v[i].y;
+            o[2 * i * kQS + 8] = s.v[i].z;
+            o[2 * i * kQS + 12] = s.v[i].w;
+        }
+    }
+    __device__ static void stager_regs(const SegDesc& d, const float* __restrict__ E, float* lds, int nch) {
+        static_assert(VS == 32, "register staging is for 32-float rows");
+        const int T = d.T;
+        auto buf = [&](int q) { return lds + (q % kBufs) * kBufFloats; };
+        StgSet s0, s1, s2, s3;
+        stg_load(s0, E, T, 0);
+        stg_load(s1, E, T, 1);
+        stg_load(s2, E, T, 2);
+        stg_load(s3, E, T, 3);
+        stg_write(s0, buf(0));
+        stg_write(s1, buf(1));
+        stg_load(s0, E, T, 4);
+        stg_load(s1, E, T, 5);
+        __syncthreads();  // barrier -1
+        // iteration q: chunk q + 2 (set (q + 2) % 4) into its quad buffer, then chunk q + 6 into
+        // that set; barrier q
+        auto iter = [&](int q, StgSet& s) {
+            if (q + 2 < nch) stg_write(s, buf(q + 2));
+            stg_load(s, E, T, q + 6);
+            __syncthreads();  // barrier q
+        };
+        int q = 0;
+        for (; q + 4 <= nch; q += 4) {
+            iter(q, s2);
+            iter(q + 1, s3);
+            iter(q + 2, s0);
+            iter(q + 3, s1);
+        }
+        if (q < nch) iter(q++, s2);
+        if (q < nch) iter(q++, s3);
+        if (q < nch) iter(q++, s0);
+        wait_vm();  // (no load outlives the wave)
+    }
+
     __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* raw,
                                       int nch, int tok0, bool col0, bool stage, bool x4) {
         const int T = d.T;
+        if constexpr (VS == 32) {
+            if (stage && x4 && !col0) {
+                stager_regs(d, E, lds, nch);
+                return;
+            }
+        }
         auto buf = [&](int q) { return lds + (q % kBufs) * kBufFloats; };
         auto ring = [&](int q) { return raw + (q % kRing) * kChunk * VS; };
         auto rows_of = [&](int q) { return (q >= 0 && q < nch) ? min(kChunk, T - q * kChunk) : 0; };
@@ -957,26 +1004,31 @@ struct Forward {
             if (q < nch) stage_rows<VS, 1, true>(E, V, q * kChunk, rows_of(q), ring(q), x4, cm);
         };
         // waits by DMA instruction count (stage_rows: one 16-byte instruction per 8 rows, else one
-        // per row)
-        auto wait_all_but = [&](int q) {  // all but chunk q's DMA instructions landed
-            const int n = q < nch ? (x4 && VS == 32 ? (rows_of(q) + 7) / 8 : rows_of(q)) : 0;
-            if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        // per row); the loads complete in order, so "at most n in flight" = everything but the
+        // newest n landed
+        auto instrs = [&](int q) { return q < nch ? (x4 && VS == 32 ? (rows_of(q) + 7) / 8 : rows_of(q)) : 0; };
+        auto wait_all_but = [&](int q0, int q1) {  // all but chunks [q0, q1)'s DMA instructions landed
+            int n = 0;
+            for (int c = q0; c < q1; ++c) n += instrs(c);
+            if (n >= 60) asm volatile("s_waitcnt vmcnt(60)" ::: "memory");
+            else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
             else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
             else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         };
         if (stage) {
             for (int q = 0; q < kRing - 1; ++q) issue(q);
-            wait_vm();
+            wait_all_but(2, kRing - 1);  // chunks 0 and 1 landed
             transpose_quads(ring(0), buf(0));
             if (nch > 1) transpose_quads(ring(1), buf(1));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot 0's reads done before its reuse
             issue(kRing - 1);
         }
         double acc = 0.0;
-#ifdef WX_HELPER_PRIO
-        if (col0) __builtin_amdgcn_s_setprio(WX_HELPER_PRIO);
-#endif
         __syncthreads();  // barrier -1
         if (col0) {
             col0_pre(0, d, buf(0), tok0, acc);
@@ -990,8 +1042,14 @@ struct Forward {
         // chunk q, transposed two iterations ago), barrier q, column 0
         for (int q = 0; q < nch; ++q) {
             WX_T(h0);
+#ifdef WX_PHASE_TIMING
+            unsigned long long hw = h0;
+#endif
             if (stage && q + 2 < nch) {
-                wait_all_but(q + 3);  // chunk q + 2's DMA landed (q + 3's may be in flight)
+                wait_all_but(q + 3, q + kRing);  // chunk q + 2's DMA landed (later ones may be in flight)
+#ifdef WX_PHASE_TIMING
+                hw = __builtin_amdgcn_s_memtime();
+#endif
                 transpose_quads(ring(q + 2), buf(q + 2));
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads done: the slot is free
                 issue(q + kRing);
@@ -1002,13 +1060,13 @@ struct Forward {
             if (col0 && q + 2 < nch) col0_pre(q + 2, d, buf(q + 2), tok0, acc);
             WX_T(h3);
 #ifdef WX_PHASE_TIMING
-            acc_vm += h1 - h0;
+            acc_vm += hw - h0;
             acc_bar += h2 - h1;
-            acc_work += h3 - h2;
+            acc_work += (h3 - h2) + (h1 - hw);
 #endif
         }
 #ifdef WX_PHASE_TIMING
-        if (lane_id() == 0 && blockIdx.x < 8192) {  // [work, barrier wait, vmcnt wait] per helper
+        if (lane_id() == 0 && blockIdx.x < 8192) {  // [work, barrier wait, DMA wait] per helper
             unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W + (stage ? 0 : 1)) * 3;
             o[0] = acc_work;
             o[1] = acc_bar;
@@ -1496,48 +1554,14 @@ __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bit
     return row[(unsigned)(k * lay.lanes + g)];
 }
 
-// Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d; steps
-// before the walk's start must have their bits cleared.  The block's bit columns are first
-// transposed into SGPR ballots (mask_s bit i = decision bit of window lane i at step s), so
-// the serial part is a pure SALU chain per step — SCC = mask_s[d]; d += SCC — with no
-// VALU <-> SALU round trip.  Returns the change mask (bit 31-s = the path moved onto a new
-// token at 32b+s).
-__device__ __forceinline__ unsigned walk_block(unsigned win, int& d) {
-    unsigned cm = 0u;
-#pragma unroll
-    for (int s0 = 31; s0 >= 0; s0 -= 8) {
-        unsigned long long m[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = __ballot((win >> (31 - (s0 - i))) & 1u);
-        // all 8 ballots are issued before the chain reads the first (hipcc would otherwise
-        // sink each v_cmp next to its reader and expose the VALU -> SGPR latency per step)
-        asm volatile("" ::"s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(m[4]), "s"(m[5]), "s"(m[6]), "s"(m[7]));
-        unsigned t0, t1;
-#define WX_WALK_STEP(I, T)                        \
-    "s_bitcmp1_b64 %[m" #I "], %[d]\n\t"          \
-    "s_cselect_b32 %[" #T "], %[k" #I "], 0\n\t" \
-    "s_addc_u32 %[d], %[d], 0\n\t"                \
-    "s_or_b32 %[cm], %[cm], %[" #T "]\n\t"
-        asm volatile(WX_WALK_STEP(0, t0) WX_WALK_STEP(1, t1) WX_WALK_STEP(2, t0) WX_WALK_STEP(3, t1)
-                         WX_WALK_STEP(4, t0) WX_WALK_STEP(5, t1) WX_WALK_STEP(6, t0) WX_WALK_STEP(7, t1)
-                     : [d] "+s"(d), [cm] "+s"(cm), [t0] "=&s"(t0), [t1] "=&s"(t1)
-                     : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3]), [m4] "s"(m[4]),
-                       [m5] "s"(m[5]), [m6] "s"(m[6]), [m7] "s"(m[7]), [k0] "i"(1u << (31 - s0)),
-                       [k1] "i"(1u << (32 - s0)), [k2] "i"(1u << (33 - s0)), [k3] "i"(1u << (34 - s0)),
-                       [k4] "i"(1u << (35 - s0)), [k5] "i"(1u << (36 - s0)), [k6] "i"(1u << (37 - s0)),
-                       [k7] "i"(1u << (38 - s0))
-                     : "scc");
-#undef WX_WALK_STEP
-    }
-    return cm;
-}
-
-// Run-length form of walk_block: one iteration per token change instead of per step.
-// The path stays on window lane d until the next set bit (in walking order: increasing
-// bit position) of that lane's word, moves there, and continues from the next step on
-// lane d+1.  A successful path makes exactly N changes, so the serial chain costs
-// ~N * (readlane + 8 SALU) per segment instead of T * 4 SALU + the ballot transposes.
-// Same contract as walk_block: bits of steps before the walk's start are cleared.
+// Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d, run-length
+// form: one iteration per token change instead of per step.  The path stays on window lane
+// d until the next set bit (in walking order: increasing bit position) of that lane's word,
+// moves there, and continues from the next step on lane d+1.  A successful path makes
+// exactly N changes, so the serial chain costs ~N * (readlane + 8 SALU) per segment instead
+// of T * 4 SALU (a per-step ballot-transposed SALU chain, replaced in round 2).  Bits of
+// steps before the walk's start must be cleared.  Returns the change mask (bit 31-s = the
+// path moved onto a new token at 32b+s).
 __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
     // Per change: x = word[dd] & m (m: bit positions still ahead) is non-zero; p = its lowest
     // set bit is the change; m = -2 << p keeps the positions after it (0 after bit 31: the
@@ -1687,9 +1711,6 @@ __device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsi
         win &= first_mask;
         first_mask = 0xFFFFFFFFu;
         const int d0 = dd;
-#ifdef WX_WALK_BALLOT
-        const unsigned cm = walk_block(win, dd);
-#else
 #ifdef WX_PHASE_TIMING
         WX_T(rl0);
 #endif
@@ -1699,7 +1720,6 @@ __device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsi
         t_rl += rl1 - rl0;
         n_ch += __popc(cm);
         ++n_bl;
-#endif
 #endif
         // change masks are collected in lane b % 64 and stored 64 blocks at a time, through
         // an explicit LDS or global store (a flat store in the loop makes hipcc drain every
@@ -1794,17 +1814,9 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
 // Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
 // block, or -1), meaningful in wave 0.
 constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
-#ifndef WX_SPEC_OVERLAP
-#define WX_SPEC_OVERLAP 2
-#endif
-constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker starts above its segment
-#ifndef WX_SPEC_EARLY
-#define WX_SPEC_EARLY 1
-#endif
-#ifndef WX_SPEC_ARGMAX_BLOCKS
-#define WX_SPEC_ARGMAX_BLOCKS 3
-#endif
-constexpr int kSpecArgmaxBlocks = WX_SPEC_ARGMAX_BLOCKS;  // wave 0's t_start search, in walk blocks
+constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment
+// wave 0's t_start search, in walk blocks (A/B: 1, 3 or 5 within noise)
+constexpr int kSpecArgmaxBlocks = 3;
 template <int CC>
 __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int T, const float* cn,
                          int* argred, unsigned* cmask, int K, int* colrec, int* sbuf, int& t_start) {
@@ -1819,21 +1831,14 @@ __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, i
     sw.send = sbuf + 2 * K;
     int res = -1, jo = 0, tb = 0;
     unsigned fm = 0u;
-#if WX_SPEC_EARLY
     // The segments cover the blocks below T (t_start <= T): the walkers start while wave 0
-    // alone finds t_start, so its segment is kSpecArgmaxBlocks shorter than theirs.
+    // alone finds t_start, so its segment is kSpecArgmaxBlocks shorter than theirs.  (Round 2
+    // waited for a workgroup-wide t_start first: 1-2 us slower.)
     sw.top = (T - 1) >> 5;
     sw.L = max((sw.top + 1 + kSpecArgmaxBlocks + K - 1) / K, 1);
     sw.L0 = max(sw.L - kSpecArgmaxBlocks, 1);
     const int tref = T;
     if (wv == 0) t_start = column_argmax(cn, T);
-#else
-    t_start = block_argmax(cn, T, argred);
-    sw.top = (t_start - 1) >> 5;
-    sw.L = max((sw.top + 1 - kSpecOverlap + K - 1) / K, 1);
-    sw.L0 = sw.L + kSpecOverlap;  // (balances wave 0's segment with the walkers' overlap + segment)
-    const int tref = t_start;
-#endif
     if (wv == 0) {
         if (t_start <= 0) {
             res = -1;  // (the reference's None)
@@ -1973,6 +1978,8 @@ __host__ __device__ __forceinline__ int bucket_cells_total(int id) { return buck
 // Split buckets (C cells per lane, W DP waves + 1 helper per part, P parts): the chunk
 // halo runs through all W * P virtual waves.  Segments too long for the widest split bucket
 // use the single-CU latency buckets in the same launch.
+// (A/B, config 2: 5 DP waves per part instead of 4 were 2 us slower, 6 — two hand-off hops
+// fewer — 0.8 us faster, though the DP waves sharing a SIMD slow each other's chains.)
 #define WX_SPLIT_BUCKETS(X) X(1, 3) X(1, 4) X(2, 3) X(4, 3)
 constexpr int kSplitFlag = 1 << 20;
 __host__ __device__ constexpr int split_capacity(int C, int W, int P) {
@@ -2242,7 +2249,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 }
 
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu((WX_PIPE_C8W && C == 8 && W > 1 && !H && VS != kGatherVS) ? 4 : 1, H ? 2 : 8))) void align_dp_kernel(
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
 }
@@ -3688,6 +3695,9 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
         !workspace)
         return WX_E_INVALID;
     if (V < 1 || V > WX_MAX_VOCAB) return WX_E_VOCAB;
+#ifdef WX_DEV_V32
+    if (V > 32) return WX_E_INVALID;  // development build: only the V <= 32 kernels exist
+#endif
     if (max_N > WX_MAX_TOKENS) return WX_E_TOO_LONG;
     if (workspace_bytes < wx_align_dp_workspace_bytes(S, sum_T, max_N)) return WX_E_WORKSPACE;
     if (handoff && handoff_bytes < wx_align_dp_handoff_bytes(S, sum_T)) return WX_E_WORKSPACE;
@@ -3771,6 +3781,9 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V, const int32_t*
     if (S == 0) return WX_OK;
     if (!em || !em_off || !tok_off || !blank_id || !trellis || !tr_off) return WX_E_INVALID;
     if (V < 1 || V > WX_MAX_VOCAB) return WX_E_VOCAB;
+#ifdef WX_DEV_V32
+    if (V > 32) return WX_E_INVALID;  // development build: only the V <= 32 kernels exist
+#endif
     if (max_N > WX_MAX_TOKENS) return WX_E_TOO_LONG;
     TrellisArgs a;
     a.em = em; a.em_off = em_off; a.V = V; a.tok = tok; a.tok_off = tok_off; a.blank_id = blank_id;
@@ -3952,6 +3965,10 @@ extern "C" int wx_vad_aggregate(const float* scores, const int64_t* start_frame,
 #ifdef WX_PHASE_TIMING
 extern "C" int wx_debug_phases(unsigned long long* host, int n) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_phase), sizeof(unsigned long long) * 6 * (size_t)n, 0,
+                                    hipMemcpyDeviceToHost);
+}
+extern "C" int wx_debug_cq(unsigned long long* host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_cq), sizeof(unsigned long long) * 48 * 3 * (size_t)n, 0,
                                     hipMemcpyDeviceToHost);
 }
 extern "C" int wx_debug_loop(unsigned long long* host, int n) {

@@ -116,11 +116,6 @@ struct AttnArgs {
     int B, H, T;
     int64_t sqb, sqh, sqt, skb, skh, skt, svb, svh, svt;  // element strides (head dim: 1)
     float scale_log2;                                      // softmax scale * log2(e)
-    // ragged batch (wx_attention_f32_csr): segment s = rows [row_off[s], row_off[s+1]) of
-    // [sum_T, H, 64] q/k/v/o, its query tiles [tile_off[s], tile_off[s+1]) of blockIdx.x
-    const int64_t* row_off;  // nullptr: the uniform [B, H, T, 64] form
-    const int32_t* tile_off;
-    int S;
 };
 
 #ifndef WX_ATTN_SPLIT
@@ -129,36 +124,14 @@ struct AttnArgs {
 constexpr int kAttnSplit = WX_ATTN_SPLIT;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
 
 __global__ __launch_bounds__(64 * kAttnSplit) void attn_f32_kernel(AttnArgs a) {
-    int T, q0, h;
-    int64_t row0;  // o row of query 0 of this batch entry / segment
-    const float *Q, *K, *V;
-    if (a.row_off) {  // ragged: the segment owning this query tile (the last with tile_off <= x)
-        const int x = (int)blockIdx.x;
-        int lo = 0, hi = a.S - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (a.tile_off[mid] <= x)
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-        row0 = a.row_off[lo];
-        T = (int)(a.row_off[lo + 1] - row0);
-        q0 = (x - a.tile_off[lo]) * 32;
-        h = blockIdx.y;
-        Q = a.q + row0 * a.sqt + h * a.sqh;
-        K = a.k + row0 * a.skt + h * a.skh;
-        V = a.v + row0 * a.svt + h * a.svh;
-    } else {
-        T = a.T;
-        q0 = blockIdx.x * 32;
-        const int b = blockIdx.y / a.H;
-        h = blockIdx.y % a.H;
-        row0 = (int64_t)b * T;
-        Q = a.q + b * a.sqb + h * a.sqh;
-        K = a.k + b * a.skb + h * a.skh;
-        V = a.v + b * a.svb + h * a.svh;
-    }
+    const int T = a.T;
+    const int q0 = blockIdx.x * 32;
+    const int b = blockIdx.y / a.H;
+    const int h = blockIdx.y % a.H;
+    const int64_t row0 = (int64_t)b * T;  // o row of query 0 of this batch entry
+    const float* Q = a.q + b * a.sqb + h * a.sqh;
+    const float* K = a.k + b * a.skb + h * a.skh;
+    const float* V = a.v + b * a.svb + h * a.svh;
     const int l = threadIdx.x & 63, r = l & 31, hf = l >> 5, wv = threadIdx.x >> 6;
     float qv[32];
     {
@@ -354,50 +327,7 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     a.svh = v_strides[1];
     a.svt = v_strides[2];
     a.scale_log2 = scale * 1.4426950408889634f;
-    a.row_off = nullptr;
-    a.tile_off = nullptr;
-    a.S = 0;
     hipLaunchKernelGGL(attn_f32_kernel, dim3((unsigned)((T + 31) / 32), (unsigned)(B * H)), dim3(64 * kAttnSplit), 0,
-                       reinterpret_cast<hipStream_t>(stream), a);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? WX_OK : (int)e;
-}
-
-extern "C" int wx_attention_f32_csr(const float* q, const float* k, const float* v, float* o, int32_t S, int32_t H,
-                                    int32_t D, const int64_t* row_off, const int32_t* tile_off, int32_t n_tiles,
-                                    const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
-                                    float scale, void* stream) {
-    using namespace wxe;
-    if (S < 0 || H <= 0 || n_tiles < 0 || D != 64 || !q || !k || !v || !o || !q_strides || !k_strides ||
-        !v_strides || (S > 0 && (!row_off || !tile_off)))
-        return WX_E_INVALID;
-    if (S == 0 || n_tiles == 0) return WX_OK;
-    const int64_t* st[3] = {q_strides, k_strides, v_strides};
-    const float* pt[3] = {q, k, v};
-    for (int i = 0; i < 3; ++i) {
-        if ((reinterpret_cast<uintptr_t>(pt[i]) & 15) || (st[i][0] & 3) || (st[i][1] & 3)) return WX_E_INVALID;
-    }
-    if (reinterpret_cast<uintptr_t>(o) & 15) return WX_E_INVALID;
-    AttnArgs a;
-    a.q = q;
-    a.k = k;
-    a.v = v;
-    a.o = o;
-    a.B = 0;
-    a.H = H;
-    a.T = 0;
-    a.sqb = a.skb = a.svb = 0;
-    a.sqt = q_strides[0];
-    a.sqh = q_strides[1];
-    a.skt = k_strides[0];
-    a.skh = k_strides[1];
-    a.svt = v_strides[0];
-    a.svh = v_strides[1];
-    a.scale_log2 = scale * 1.4426950408889634f;
-    a.row_off = row_off;
-    a.tile_off = tile_off;
-    a.S = S;
-    hipLaunchKernelGGL(attn_f32_kernel, dim3((unsigned)n_tiles, (unsigned)H), dim3(64 * kAttnSplit), 0,
                        reinterpret_cast<hipStream_t>(stream), a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;

@@ -40,7 +40,7 @@ import contextlib
 import os
 import threading
 import types
-from typing import List, Optional, Sequence
+from typing import Optional
 
 import torch
 import torch.nn.functional as F
@@ -292,79 +292,6 @@ def prepared(model: torch.nn.Module):
                 if model.__dict__.pop("_wx_prep_owned", False):
                     restore_model(model)
                 del model.__dict__["_wx_prep_refs"]
-
-
-def batchable(model) -> bool:
-    """Whether align() runs `model` through batched_logits: opt-in (WX_EMISSION_BATCH=G > 0,
-    G segments per batch), for an HF Wav2Vec2ForCTC (base / post-norm or stable-layer-norm
-    encoder, no adapter) with 64-wide heads, in eval mode.  Off by default: on MI355X the
-    per-segment forwards on 8 streams already overlap enough that batching gains nothing
-    (16 x 30 s, steady state: 105.9 ms per-segment vs 104.8-120.1 ms batched at G = 16..2;
-    config 3 slower at G = 8), the fp32 matrix work being the bound."""
-    w2v = getattr(model, "wav2vec2", None)
-    cfg = getattr(model, "config", None)
-    if int(os.environ.get("WX_EMISSION_BATCH", "0") or 0) <= 0 or os.environ.get("WX_NO_BATCH"):
-        return False
-    if w2v is None or cfg is None or model.training:
-        return False
-    enc = getattr(w2v, "encoder", None)
-    if enc is None or getattr(w2v, "adapter", None) is not None or not hasattr(model, "lm_head"):
-        return False
-    heads = int(getattr(cfg, "num_attention_heads", 0) or 0)
-    return heads > 0 and int(cfg.hidden_size) == 64 * heads
-
-
-def _self_attention(att, h: torch.Tensor, Ts) -> torch.Tensor:
-    """Wav2Vec2Attention (no mask, eval) over the rows of a ragged batch: the q/k/v/out
-    projections on all rows at once, wx_attention_f32_csr within each segment."""
-    from . import _lib
-
-    R = h.shape[0]
-    H = att.num_heads
-    q = att.q_proj(h).view(R, H, 64)
-    k = att.k_proj(h).view(R, H, 64)
-    v = att.v_proj(h).view(R, H, 64)
-    o = _lib.attention_f32_csr(q, k, v, Ts, att.scaling)
-    return att.out_proj(o.view(R, H * 64))
-
-
-def batched_logits(model, waveforms) -> List[torch.Tensor]:
-    """The HF Wav2Vec2ForCTC forward of every waveform (alignment.py:226-232), batched
-    without padding: the convolutional feature encoder and the positional convolution run per
-    segment (they mix frames in time), every row-wise op (layer norms, projections, feed
-    forward, lm_head) runs once on the segments' concatenated frames, and the attention runs per
-    segment inside one wx_attention_f32_csr launch.  Each segment's logits equal its own
-    unpadded forward up to the GEMMs' float noise (their row count changes hipBLASLt's kernel):
-    the GEMMs of a 30 s segment (1,499 rows) fill a fraction of the GPU, those of the batch do
-    not.  Returns [T_i, V] logits per waveform."""
-    w2v = model.wav2vec2
-    cfg = model.config
-    enc = w2v.encoder
-    with torch.inference_mode():
-        feats = [w2v.feature_extractor(w.reshape(1, -1))[0].transpose(0, 1) for w in waveforms]  # [T_i, C]
-        Ts = [int(f.shape[0]) for f in feats]
-        h, _ = w2v.feature_projection(torch.cat(feats, 0))
-        pos, o = [], 0
-        for t in Ts:
-            pos.append(enc.pos_conv_embed(h[o:o + t].unsqueeze(0))[0])
-            o += t
-        h = h + torch.cat(pos, 0)
-        stable = bool(getattr(cfg, "do_stable_layer_norm", False))
-        if not stable:
-            h = enc.layer_norm(h)
-        for layer in enc.layers:
-            if stable:
-                h = h + _self_attention(layer.attention, layer.layer_norm(h), Ts)
-                h = h + layer.feed_forward(layer.final_layer_norm(h))
-                if getattr(layer, "adapter_layer", None) is not None:
-                    h = h + layer.adapter_layer(h)
-            else:
-                h = layer.layer_norm(h + _self_attention(layer.attention, h, Ts))
-                h = layer.final_layer_norm(h + layer.feed_forward(h))
-        if stable:
-            h = enc.layer_norm(h)
-        logits = model.lm_head(h)
-    return list(torch.split(logits, Ts, 0))
 
 
 def n_frames(n_samples: int, model: Optional[torch.nn.Module] = None) -> int:
