@@ -19,6 +19,8 @@
  *                        self-attention, fp32)
  *   wx_vad_aggregate  <- whisperx/vad.py:198-240 VoiceActivitySegmentation.apply's
  *                        segmentation overlap-add (pyannote Inference.aggregate)
+ *   wx_sincnet_stage  <- whisperx/vad.py:198-240 (the segmentation model's SincNet stages:
+ *                        |.| / max-pool / instance norm / leaky ReLU, fused)
  *
  * Conventions
  *   - All data pointers are DEVICE pointers (allocated by the caller; the library never
@@ -225,6 +227,16 @@ int wx_channel_norm(const float* x, int64_t L, int32_t C, const float* gamma, co
 int wx_attention_f32(const float* q, const float* k, const float* v, float* o, int32_t B, int32_t H, int32_t T,
                      int32_t D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                      float scale, void* stream);
+
+/* VAD producer (vad.py:198-240 -> pyannote SincNet): the epilogue of one SincNet stage on the
+ * time-major conv output x [B windows][L][C] (window stride x_window_stride elements, row
+ * stride C; C % 4 == 0, C <= 128, 16-byte aligned): y[b][t][c] = leaky_relu(InstanceNorm1d(
+ * MaxPool1d(3, 3)((|)x(|)))) with |.| when do_abs (the sinc filterbank stage), the norm's
+ * biased variance over the L / 3 pooled rows, eps and affine gamma/beta (may be NULL), and
+ * negative slope `slope`.  y is [B][L / 3][C] contiguous.  Statistics in fp64. */
+int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
+                     int32_t do_abs, const float* gamma, const float* beta, float eps, float slope,
+                     float* y, void* stream);
 
 /* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
  * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32

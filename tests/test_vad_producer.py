@@ -91,3 +91,59 @@ def test_vad_producer_end_to_end_device_scores():
     regions = oracle.binarize(exp, sw.start, sw.step, sw.duration, med, med, 30)
     ref = oracle.merge_chunks_regions(regions, 30)
     assert [(c["start"], c["end"]) for c in dev_chunks] == [(c["start"], c["end"]) for c in ref]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,C,do_abs,stride_pad", [(3, 7975, 80, True, 0), (5, 2654, 60, False, 4),
+                                                      (2, 880, 60, False, 4), (1, 4, 8, True, 0), (4, 2, 4, False, 0)])
+def test_sincnet_stage_vs_torch(B, L, C, do_abs, stride_pad):
+    """wx_sincnet_stage against torch's |.| -> MaxPool1d(3, 3) -> InstanceNorm1d(affine) ->
+    LeakyReLU on the same time-major input (fp32 reference of the same ops; statistics in
+    fp64 here, fp32 in MIOpen: tolerance 2e-5), windows with a row-padded stride (the k = 5
+    GEMM convs' output view), NaN propagation through the max-pool, L not a multiple of 3."""
+    from whisperx_amd import _lib
+
+    torch.manual_seed(L + C)
+    full = torch.randn(B, L + stride_pad, C, device="cuda") * 3 + torch.randn(1, 1, C, device="cuda")
+    x_tm = full[:, :L]
+    if B > 1 and L > 30:
+        x_tm[1, 10, 2] = float("nan")  # -> pooled row 3 channel 2 NaN -> that window/channel NaN
+    norm = torch.nn.InstanceNorm1d(C, affine=True).cuda()
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(C) * 0.5 + 1)
+        norm.bias.copy_(torch.randn(C) * 0.1)
+        xc = x_tm.transpose(1, 2)
+        ref = torch.nn.functional.leaky_relu(norm(torch.nn.functional.max_pool1d(xc.abs() if do_abs else xc, 3, 3)))
+    got = _lib.sincnet_stage(x_tm, do_abs, norm.weight, norm.bias, norm.eps)
+    assert got.shape == (B, L // 3, C)
+    torch.testing.assert_close(got.transpose(1, 2), ref, rtol=2e-5, atol=2e-5, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_sincnet_fused_epilogue_matches_torch_ops(monkeypatch):
+    """PyanNet's forward with the fused SincNet epilogues against the same forward through
+    torch's ops (WX_NO_SINC_EPILOGUE=1), both on the GEMM route: scores within float noise, and
+    merge_chunks of the aggregated scores identical."""
+    from whisperx_amd.vad import merge_chunks
+    from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+    torch.manual_seed(1)
+    vad = VoiceActivitySegmentation(device="cuda:0", batch_size=64)
+    wav = torch.randn(1, 90 * 16000 + 77) * 0.1
+    monkeypatch.delenv("WX_NO_SINC_EPILOGUE", raising=False)
+    fused = vad.chunk_scores(wav)
+    feat_f = vad({"waveform": wav, "sample_rate": 16000})
+    monkeypatch.setenv("WX_NO_SINC_EPILOGUE", "1")
+    plain = vad.chunk_scores(wav)
+    feat_p = vad({"waveform": wav, "sample_rate": 16000})
+    diff = (fused - plain).abs().max().item()
+    assert diff <= 2e-5
+    # scores this close give the same chunks unless a frame sits on the threshold: binarise at
+    # the middle of the widest gap between the sorted frame scores (5th to 95th percentile)
+    vals = np.sort(feat_p.data[:, 0].cpu().numpy())
+    vals = vals[np.isfinite(vals)]
+    lo, hi = len(vals) // 20, 19 * len(vals) // 20
+    i = lo + int(np.argmax(np.diff(vals[lo:hi + 1])))
+    thr = float(0.5 * (vals[i] + vals[i + 1]))
+    if vals[i + 1] - vals[i] > 4 * diff:  # (every frame on the same side of thr in both)
+        assert merge_chunks(feat_f, 30, onset=thr, offset=thr) == merge_chunks(feat_p, 30, onset=thr, offset=thr)

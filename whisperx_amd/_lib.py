@@ -21,7 +21,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WX_LIB_PATH") or os.path.join(_HERE, "libwxalign.so")
 SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
-SRC_PATHS = [SRC_PATH, os.path.join(_HERE, "csrc", "wx_emission.hip")]
+SRC_PATHS = [SRC_PATH, os.path.join(_HERE, "csrc", "wx_emission.hip"), os.path.join(_HERE, "csrc", "wx_vad.hip")]
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 MAX_VOCAB = 16384
@@ -82,6 +82,7 @@ SIGNATURES = {
     "wx_binarize_ex": (ctypes.c_int, [_vp, _vp, _i32, _i64, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                       _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "wx_binarize_plan": (ctypes.c_int, [_f32, _f32, _i64, ctypes.c_char_p, _sz]),
+    "wx_sincnet_stage": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _f32, _f32, _vp, _vp]),
 }
 
 
@@ -489,6 +490,22 @@ def vad_aggregate(scores: torch.Tensor, start_frames, n_frames: int, missing: fl
         _check(lib.wx_vad_aggregate(_ptr(sc), _ptr(sf), n_chunks, K, n_cls, int(n_frames), float(missing),
                                     _ptr(out), _stream(dev)))
     return out[: int(n_frames)]
+
+
+def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slope: float = 0.01) -> torch.Tensor:
+    """wx_sincnet_stage on a time-major conv output x_tm [B, L, C] (row stride C, any window
+    stride): leaky_relu(InstanceNorm1d(MaxPool1d(3, 3)(|x|?))) as [B, L // 3, C] contiguous."""
+    lib = load()
+    B, L, C = (int(v) for v in x_tm.shape)
+    if x_tm.dtype != torch.float32 or x_tm.stride(2) != 1 or x_tm.stride(1) != C:
+        raise WXError("sincnet_stage: x must be float32 [B, L, C] with contiguous rows")
+    y = torch.empty((B, L // 3, C), dtype=torch.float32, device=x_tm.device)
+    g = gamma.detach().contiguous() if gamma is not None else None
+    bt = beta.detach().contiguous() if beta is not None else None
+    with torch.cuda.device(x_tm.device):
+        _check(lib.wx_sincnet_stage(_ptr(x_tm), B, L, C, int(x_tm.stride(0)), int(bool(do_abs)), _ptr(g), _ptr(bt),
+                                    float(eps), float(slope), _ptr(y), _stream(x_tm.device)))
+    return y
 
 
 def channel_norm(x: torch.Tensor, gamma, beta, eps: float, gelu: bool, out: Optional[torch.Tensor] = None):

@@ -31,6 +31,9 @@ PyTorch-ROCm model call, one per segment, but:
   wx_attention_f32 (a flash-attention forward, one wave per 32-query tile; see
   csrc/wx_emission.hip) via transformers' attention interface; torch's fused fp32 attention
   was a third of config 3's GPU time.
+* **One q/k/v GEMM.**  Each self-attention's three projections run as one GEMM on the
+  concatenated weights (cached per call); k_proj / v_proj return column slices of its output,
+  which wx_attention_f32 reads in place (strided views).
 * **No concatenation copy.**  ``log_softmax`` writes each segment's ``[T, V]`` rows straight
   into its slice of the CSR emission matrix the DP kernel reads (``emissions_csr``).
 """
@@ -77,6 +80,8 @@ def materialize_weights(model: torch.nn.Module) -> None:
         for mod in model.modules():
             if isinstance(mod, torch.nn.Conv1d) and hasattr(mod, "_wx_orig_forward"):
                 _weight(mod)
+            if "_wx_qkv" in mod.__dict__ and next(mod.parameters()).is_cuda:
+                _qkv_weights(mod)
 
 
 def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
@@ -223,12 +228,82 @@ def _use_wx_attention(model: torch.nn.Module) -> None:
         pass
 
 
+_QKV_TLS = threading.local()  # the fused projection's k / v results until k_proj / v_proj take them
+
+
+def _qkv_weights(q: torch.nn.Linear):
+    """The attention's [Wq; Wk; Wv] (and biases) concatenated, cached until a parameter
+    changes (filled by materialize_weights on the caller's stream before any fan-out)."""
+    st = q.__dict__["_wx_qkv"]
+    k, v = st["k"], st["v"]
+    params = [m.weight for m in (q, k, v)] + [m.bias for m in (q, k, v) if m.bias is not None]
+    key = tuple((p.data_ptr(), p._version) for p in params)
+    c = st.get("cache")
+    if c is None or c[0] != key:
+        with torch.no_grad():
+            w = torch.cat([q.weight, k.weight, v.weight], 0).detach().contiguous()
+            b = torch.cat([q.bias, k.bias, v.bias]).detach() if all(m.bias is not None for m in (q, k, v)) else None
+        c = (key, w, b)
+        st["cache"] = c
+    return c[1], c[2]
+
+
+def _fused_q_forward(self, x):
+    """q_proj of a self-attention layer: one GEMM for q, k and v (768 -> 2304 for wav2vec2-base,
+    1024 -> 3072 for large) instead of three narrow ones; k_proj / v_proj then return their
+    column slices of the same output when called on the same input (Wav2Vec2Attention calls
+    them right after q_proj).  The slices are strided views (row stride 3D) that the attention
+    kernel reads in place."""
+    st = self.__dict__["_wx_qkv"]
+    if x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.float32:
+        w, b = _qkv_weights(self)
+        y = F.linear(x, w, b)
+        dq, dk = self.out_features, st["k"].out_features
+        _QKV_TLS.pending = (st["k"], x, y[..., dq:dq + dk], st["v"], y[..., dq + dk:])
+        return y[..., :dq]
+    _QKV_TLS.pending = None
+    return self._wx_orig_forward(x)
+
+
+def _fused_k_forward(self, x):
+    p = getattr(_QKV_TLS, "pending", None)
+    if p is not None and p[0] is self and p[1] is x:
+        return p[2]
+    return self._wx_orig_forward(x)
+
+
+def _fused_v_forward(self, x):
+    p = getattr(_QKV_TLS, "pending", None)
+    _QKV_TLS.pending = None
+    if p is not None and p[3] is self and p[1] is x:
+        return p[4]
+    return self._wx_orig_forward(x)
+
+
+def _fuse_qkv(model: torch.nn.Module) -> None:
+    """Route every self-attention's q/k/v projections through one fused GEMM (WX_NO_QKV=1: keep
+    three).  Applies to modules holding q_proj / k_proj / v_proj Linears of equal input width."""
+    if os.environ.get("WX_NO_QKV"):
+        return
+    for mod in model.modules():
+        q, k, v = (getattr(mod, n, None) for n in ("q_proj", "k_proj", "v_proj"))
+        if not all(isinstance(m, torch.nn.Linear) for m in (q, k, v)):
+            continue
+        if not (q.in_features == k.in_features == v.in_features) or any(hasattr(m, "_wx_orig_forward") for m in (q, k, v)):
+            continue
+        q.__dict__["_wx_qkv"] = {"k": k, "v": v}
+        for m, f in ((q, _fused_q_forward), (k, _fused_k_forward), (v, _fused_v_forward)):
+            m._wx_orig_forward = m.forward
+            m.forward = types.MethodType(f, m)
+
+
 def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
     """Route the model's Conv1d inference forwards through length-agnostic GEMMs and its
     self-attention through wx_attention_f32 (idempotent).  Returns the same model object."""
     if getattr(model, "_wx_gemm_conv", False):
         return model
     _use_wx_attention(model)
+    _fuse_qkv(model)
     for mod in model.modules():
         if isinstance(mod, torch.nn.Conv1d) and not hasattr(mod, "_wx_orig_forward"):
             mod._wx_orig_forward = mod.forward
@@ -259,6 +334,7 @@ def restore_model(model: torch.nn.Module) -> torch.nn.Module:
             del mod._wx_orig_forward
         if hasattr(mod, "_wx_w_cache"):
             del mod._wx_w_cache
+        mod.__dict__.pop("_wx_qkv", None)
     if "_wx_gemm_conv" in model.__dict__:
         del model._wx_gemm_conv
     if hasattr(model, "_wx_orig_attn"):

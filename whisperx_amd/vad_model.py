@@ -205,14 +205,36 @@ class SincNet(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.wav_norm1d(x)
         for i, (conv, pool, norm) in enumerate(zip(self.conv1d, self.pool1d, self.norm1d)):
-            if i > 0 and _gemm_conv(x):
+            gemm = _gemm_conv(x)
+            if i > 0 and gemm:
                 x = conv1d_batched(x, conv.weight, conv.bias, conv.stride[0])
             else:
                 x = conv(x)
+            if gemm and _fused_epilogue(pool, norm, x):
+                # |.| -> max-pool -> instance norm -> leaky ReLU in one HIP kernel on the
+                # time-major conv output (wx_sincnet_stage), returned as the [B, C, L/3] view
+                x = _lib.sincnet_stage(x.transpose(1, 2), i == 0, norm.weight, norm.bias, norm.eps).transpose(1, 2)
+                continue
             if i == 0:
                 x = torch.abs(x)
             x = F.leaky_relu(norm(pool(x)))
         return x
+
+
+def _fused_epilogue(pool, norm, x) -> bool:
+    """Whether a SincNet stage's pool / norm / activation take wx_sincnet_stage: pyannote's
+    shapes (MaxPool1d(3, 3), InstanceNorm1d using instance statistics, <= 128 channels, a
+    multiple of 4) on a time-major float32 conv output (WX_NO_SINC_EPILOGUE=1: torch's ops)."""
+    if os.environ.get("WX_NO_SINC_EPILOGUE") or x.dtype != torch.float32:
+        return False
+    if not (isinstance(pool, torch.nn.MaxPool1d) and pool.kernel_size in (3, (3,)) and pool.stride in (3, (3,))
+            and pool.padding in (0, (0,)) and pool.dilation in (1, (1,)) and not pool.ceil_mode):
+        return False
+    if not isinstance(norm, torch.nn.InstanceNorm1d) or (norm.track_running_stats and not norm.training):
+        return False
+    C = x.shape[1]
+    xt = x.transpose(1, 2)
+    return C % 4 == 0 and C <= 128 and xt.stride(2) == 1 and xt.stride(1) == C
 
 
 class PyanNet(torch.nn.Module):
