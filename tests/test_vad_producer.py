@@ -108,14 +108,24 @@ def test_sincnet_stage_vs_torch(B, L, C, do_abs, stride_pad):
     x_tm = full[:, :L]
     if B > 1 and L > 30:
         x_tm[1, 10, 2] = float("nan")  # -> pooled row 3 channel 2 NaN -> that window/channel NaN
-    norm = torch.nn.InstanceNorm1d(C, affine=True).cuda()
+    norm = torch.nn.InstanceNorm1d(C, affine=True).cuda().eval()  # inference, as pyannote runs it
     with torch.no_grad():
         norm.weight.copy_(torch.randn(C) * 0.5 + 1)
         norm.bias.copy_(torch.randn(C) * 0.1)
-        xc = x_tm.transpose(1, 2)
-        ref = torch.nn.functional.leaky_relu(norm(torch.nn.functional.max_pool1d(xc.abs() if do_abs else xc, 3, 3)))
     got = _lib.sincnet_stage(x_tm, do_abs, norm.weight, norm.bias, norm.eps)
     assert got.shape == (B, L // 3, C)
+    if L < 3:  # no pooled row (torch's max_pool1d refuses the empty output)
+        return
+    with torch.no_grad():
+        xc = x_tm.transpose(1, 2)
+        pooled = torch.nn.functional.max_pool1d(xc.abs() if do_abs else xc, 3, 3)
+        if pooled.shape[-1] > 1:
+            normed = norm(pooled)
+        else:  # (torch's instance_norm refuses one element; InstanceNorm1d's formula by hand)
+            mean = pooled.mean(-1, keepdim=True)
+            var = pooled.var(-1, unbiased=False, keepdim=True)
+            normed = (pooled - mean) / torch.sqrt(var + norm.eps) * norm.weight[:, None] + norm.bias[:, None]
+        ref = torch.nn.functional.leaky_relu(normed)
     torch.testing.assert_close(got.transpose(1, 2), ref, rtol=2e-5, atol=2e-5, equal_nan=True)
 
 

@@ -1,0 +1,6 @@
+set -o pipefail
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r4_gputests.log 2>&1 || { tail -40 gpurun_out/r4_gputests.log; exit 1; }
+tail -5 gpurun_out/r4_gputests.log
+for e in "X=1" "WX_NO_SINC_EPILOGUE=1" "X=1"; do env $e timeout -k 10 180 python tools/legs.py vad1h --steps 5 --warmup 1 2>&1 | tail -1 | sed "s/^/$e /"; done
+for e in "X=1" "WX_NO_QKV=1" "X=1"; do env $e timeout -k 10 180 python tools/legs.py e2e --steps 5 --warmup 2 2>&1 | tail -1 | sed "s/^/$e /"; done

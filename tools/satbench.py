@@ -134,6 +134,14 @@ def child(args):
                 ex = (ph[:, 5] - ph[:, 4].min()).reshape(-1, args.parts) / 100.0
                 out[case]["exit_by_part_med_us"] = [float(np.median(ex[:, i])) for i in range(args.parts)]
                 out[case]["exit_max_us"] = float(ex.max())
+                seg_exit = ex.max(axis=1)
+                Ns = np.array(b.Ns[: len(seg_exit)])
+                by = {}
+                for lo, hi in ((0, 288), (288, 416), (416, 448), (448, 1 << 30)):
+                    m = (Ns > lo) & (Ns <= hi)
+                    if m.any():
+                        by[f"N({lo},{hi}]"] = [int(m.sum()), round(float(np.median(seg_exit[m])), 2), round(float(seg_exit[m].max()), 2)]
+                out[case]["seg_exit_us_by_N(count,med,max)"] = by
             out[case]["phases_cyc_med"] = {"forward": float(np.median(fwd)), "walk": float(np.median(walk)),
                                            "merge": float(np.median(mrg)), "per_step_fwd": float(np.median(fwd)) / T,
                                            "per_step_walk": float(np.median(walk)) / T,
@@ -216,7 +224,7 @@ def main():
             print(f"  {case:9s} {v['ms_med']:9.4f} ms  {v['cells_per_s']:.3e} cells/s  frac {v['frac']:.3f}", flush=True)
             if "phases_cyc_med" in v:
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
-                for k in ("chunk_start_us_by_part_med", "granule_store_us_by_part_med", "granule_seen_us_by_part_med",
+                for k in ("seg_exit_us_by_N(count,med,max)", "chunk_start_us_by_part_med", "granule_store_us_by_part_med", "granule_seen_us_by_part_med",
                           "fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
                           "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_rl_med(cycles,changes,blocks)", "walk_split_med(argmax,walk,compact)",
                           "handoff_med(misses,wait_cyc,slack_cyc)"):

@@ -53,6 +53,11 @@ constexpr int kChunk = 32;  // emission rows per LDS buffer == bits per column w
 constexpr int kUnroll = 8;  // time steps per unrolled group
 constexpr int kMaxLdsFrames = 8192;  // segments up to this many frames keep walk state in LDS
 
+template <bool B>
+struct BoolTag {
+    static constexpr bool value = B;
+};
+
 __device__ __forceinline__ float nan_max(float a, float b) {
     // IEEE-754-2019 maximum (NaN-propagating): torch.maximum for non-zero-sign cases.
     return __builtin_elementwise_maximum(a, b);
@@ -144,6 +149,14 @@ __device__ __forceinline__ void glds_dword(const float* sbase, unsigned voff, un
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds_dst)
+                 : "memory");
+}
+// ... with device scope (sc1): the hand-off granules another CU writes (granule_load's scope)
+__device__ __forceinline__ void glds_dwordx4_sc1(const void* sbase, unsigned voff, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(uniform_ptr((const float*)sbase)), "s"(lds_dst)
                  : "memory");
 }
 __device__ __forceinline__ void glds_dwordx4(const float* sbase, unsigned voff, unsigned lds_dst) {
@@ -400,6 +413,16 @@ struct Split {
     uint64_t* xout;   // granules to part p+1 (p < P-1)
     int xstride;      // granules per chunk block of one segment boundary
     int spin;         // re-reads before a hand-off counts as lost (kMaxSpin; 0 in the recovery test)
+    // The hand-off consumer (wave 0) of a part > 0 of a register-resident kernel, unless it
+    // holds column N: it leaves its bitmap words in an LDS ring (two chunks) for the idle
+    // helper wave to store, so its only vector-memory operations in flight are the granule
+    // prefetches — issued two chunks ahead by LDS-DMA into a ring of three chunk slots (32
+    // granules each) and waited for with a hand-counted vmcnt.  (hipcc's own waits could not do
+    // this: with loads and stores both pending it waits vmcnt(0), which paid the prefetch
+    // issued a chunk earlier and the previous chunk's store round trip at every chunk.)
+    unsigned* sbits;  // LDS [2][64]
+    float* scn;       // LDS [2][32]: its column-N rows when the consumer also holds column N
+    uint64_t* xring;  // LDS [3][32]
 };
 
 __device__ __forceinline__ void granule_store(uint64_t* g, float v, unsigned tag) {
@@ -484,14 +507,22 @@ struct Forward {
 #pragma unroll
         for (int k = 0; k < C; ++k) ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
         const bool first = __all(ok);
-        for (int it = 0; !lost && !__all(ok) && it < spin; ++it) {
-            __builtin_amdgcn_s_sleep(2);
-            ok = true;
+        if (!first) {
+            for (int it = 0; !lost && !__all(ok) && it < spin; ++it) {
+                __builtin_amdgcn_s_sleep(2);
+                ok = true;
 #pragma unroll
-            for (int k = 0; k < C; ++k) {
-                xpre[k] = granule_load(gi + k);
-                ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
+                for (int k = 0; k < C; ++k) {
+                    xpre[k] = granule_load(gi + k);
+                    ok = ok && (l >= HL || (unsigned)(xpre[k] >> 32) == want);
+                }
             }
+            // The re-read loop issues a data-dependent number of loads: end it with nothing in
+            // flight, so that hipcc's waitcnt analysis still knows how many loads are pending
+            // at the next chunk's check and waits for the two-chunk-old prefetch only (an
+            // unbounded count made it wait vmcnt(0) there: the prefetch issued one chunk ago
+            // and the previous chunk's bitmap stores were waited for at every chunk).
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         }
         lost = lost || !__all(ok);
         return first;
@@ -522,7 +553,7 @@ struct Forward {
             if constexpr (kReg) {
                 int t0 = N > 0 ? tok[d.tok0] : 0;
                 t0 = (t0 >= 0 && t0 < V) ? t0 : 0;
-                helper_reg(d, E, V, lds, lds + kBufs * kBufFloats, nch, t0, col0, wv == W, x4);
+                helper_reg(d, E, V, lds, lds + kBufs * kBufFloats, nch, t0, col0, wv == W, x4, sp, bits, cn);
             } else {
                 helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
             }
@@ -554,6 +585,8 @@ struct Forward {
         // wave 0 of parts > 0 takes its halo lanes from the previous part.
         const bool xpub = SP && wv == W - 1 && sp->p + 1 < sp->P && Geo::lane_of(vw + 1, Geo::HL) < L.G;
         const bool xsub = SP && wv == 0 && sp->p > 0;
+        // (own_w, own_l below: column N's wave and lane)
+        bool route = false;
         const int f = L.first(g), cnt = L.count(g);
         const bool is_short = g < L.n_short;
         // per-slot LDS byte offsets of em[., tok[j-1]]
@@ -570,6 +603,8 @@ struct Forward {
         int own_w, own_l;
         Geo::owner(L.G - 1, own_w, own_l);
         const bool owner = uniform(own_w) == vw && l == own_l;
+        const bool owner_wave = uniform(own_w) == vw;
+        route = kReg && xsub;
 
         State st;
         if (MODE == 1) {
@@ -608,7 +643,7 @@ struct Forward {
         // segment's granule block): a lane- or chunk-conditional load merges into the old
         // value's register, and hipcc then waits for the load right where it is issued.
         const int xl = min(l, Geo::HL - 1) * C;
-        if (SP && xsub) {
+        if (SP && xsub && !route) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 xodd[k] = granule_load(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride + xl + k);
@@ -633,7 +668,13 @@ struct Forward {
         const int etq = (vw == 0 && l == 0) ? VS * 16 : toff[0] * 4;  // quad byte offset of this lane's column
         const int ebq = boff * 4;                                      // ... of the blank (uniform)
         if (kReg) __syncthreads();  // barrier -1 (helper_reg: the column-0 helper's first two chunks)
-        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C], RegOps& o, RegOps& n) {
+        // XS (compile time): the routed hand-off consumer (Split::sbits): no global store in its
+        // code path.  OWN: the wave holding column N (the only one with column-N stores; the
+        // others have no branch around them: a taken branch per eight steps cost the DP waves
+        // ~20% of their step time).
+        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C], RegOps& o, RegOps& n, auto xs, auto own) {
+            constexpr bool XS = decltype(xs)::value;
+            constexpr bool OWN = decltype(own)::value;
             WX_T(c0);
             float* buf = lds + (q % kBufs) * kBufFloats;
             const int rows = min(kChunk, T - q * kChunk);
@@ -642,10 +683,12 @@ struct Forward {
 #pragma unroll
                 for (int k = 0; k < C; ++k) xq[wv * kWave + (l - (kWave - Geo::HL)) * C + k] = st.cur[k];
             }
-            if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
-                uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
+            if constexpr (!XS) {
+                if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
+                    uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
 #pragma unroll
-                for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
+                    for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
+                }
             }
             if (SP && xpub) WX_CQ(q, 1);
             WX_T(c1);
@@ -659,6 +702,12 @@ struct Forward {
             if (W > 1 && q > 0 && halo && wv > 0) {
 #pragma unroll
                 for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
+            }
+            if constexpr (XS) {  // chunk q's DMA landed (chunk q + 1's may be in flight)
+                if (q > 0) {
+                    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                    xpre[0] = sp->xring[(q % 3) * 32 + min(l, Geo::HL - 1)];
+                }
             }
             if (SP && xsub && q > 0) {
                 // Halo of row 32q from the previous part: the granules prefetched two chunks
@@ -691,11 +740,19 @@ struct Forward {
 #endif
                 // this set's next chunk, q + 2 (the old values are dead: keep the load below)
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (XS) {
+                    if (l < 16)  // 32 granules = 16 lanes x 16 bytes into ring slot (q + 2) % 3
+                        glds_dwordx4_sc1(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride, (unsigned)l * 16u,
+                                         (unsigned)uniform((int)lds_addr(sp->xring + ((q + 2) % 3) * 32)));
+                } else {
 #pragma unroll
-                for (int k = 0; k < C; ++k)
-                    xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
+                    for (int k = 0; k < C; ++k)
+                        xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
+                }
             }
-            if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
+            if constexpr (!XS) {
+                if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
+            }
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
@@ -710,7 +767,8 @@ struct Forward {
                 // the next chunk's operands (the last chunk re-reads its own rows: harmless)
                 const char* nb = reinterpret_cast<const char*>(lds + ((q + 1 < nch ? q + 1 : q) % kBufs) * kBufFloats);
                 float cur0 = st.cur[0];
-                reg_chunk(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T);
+                reg_chunk<OWN, XS>(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T,
+                                   XS ? sp->scn + (q & 1) * kChunk : nullptr);
                 // Invariant: on a partial last chunk reg_chunk runs all 32 steps on stale rows,
                 // so st.cur then holds the cell 32 steps on, not `rows` steps: nothing reads the
                 // state after the last chunk (its bits are masked below, column N stops at T).
@@ -719,6 +777,7 @@ struct Forward {
                 st.cur[0] = cur0;
                 st.t += rows;
             } else if (vw == 0) {
+                (void)OWN;
                 chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             } else {
                 chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
@@ -737,7 +796,9 @@ struct Forward {
                     // step, the bits of the steps past T are dropped)
                     const unsigned wq = kReg ? (st.w[k] & (0xFFFFFFFFu << sh))
                                              : ((sh == 0) ? st.w[k] : (st.w[k] << sh));
-                    if (SP)
+                    if (XS)
+                        sp->sbits[(q & 1) * kWave + l] = wq;  // (C == 1)
+                    else if (SP)
                         wdef[k] = wq;
                     else if (!halo && g < L.G)  // (lanes past column N: words the walk never reads)
                         bits[((int64_t)q * C + k) * lanes + g] = wq;
@@ -746,13 +807,40 @@ struct Forward {
             }
         };
         if constexpr (SP) {
-            for (int q = 0; q < nch; q += 2) {
-                chunk_iter(q, xeven, opsA, opsB);
-                if (q + 1 < nch) chunk_iter(q + 1, xodd, opsB, opsA);
+            auto loop = [&](auto xs, auto own) {
+                for (int q = 0; q < nch; q += 2) {
+                    chunk_iter(q, xeven, opsA, opsB, xs, own);
+                    if (q + 1 < nch) chunk_iter(q + 1, xodd, opsB, opsA, xs, own);
+                }
+            };
+            if (route) {
+                // the first two chunks' granules (the plain-load path prefetches them below)
+                if (l < 16) {
+                    const unsigned base = (unsigned)uniform((int)lds_addr(sp->xring));
+                    glds_dwordx4_sc1(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride, (unsigned)l * 16u, base + 32u * 8u);
+                    glds_dwordx4_sc1(sp->xin + (int64_t)min(2, nch - 1) * sp->xstride, (unsigned)l * 16u, base + 64u * 8u);
+                }
+                if (owner_wave)
+                    loop(BoolTag<kReg>{}, BoolTag<true>{});
+                else
+                    loop(BoolTag<kReg>{}, BoolTag<false>{});
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA outlives the loop)
+                // the last two chunks' bitmap words and column-N rows (the helper stored up to
+                // chunk nch - 3)
+                for (int qd = max(nch - 2, 0); qd < nch; ++qd) {
+                    if (!halo && g < L.G) bits[(int64_t)qd * lanes + g] = sp->sbits[(qd & 1) * kWave + l];
+                    if (owner_wave && l < kChunk && qd * kChunk + l < T) cn[qd * kChunk + l] = sp->scn[(qd & 1) * kChunk + l];
+                }
+            } else if (owner_wave) {
+                loop(BoolTag<false>{}, BoolTag<true>{});
+            } else {
+                loop(BoolTag<false>{}, BoolTag<false>{});
             }
-            if (MODE == 0 && nch > 0 && !halo && g < L.G) store_deferred(nch - 1);
+            if (!route && MODE == 0 && nch > 0 && !halo && g < L.G) {
+                store_deferred(nch - 1);
+            }
         } else {
-            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB);
+            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB, BoolTag<false>{}, BoolTag<true>{});
         }
 #ifdef WX_PHASE_TIMING
         if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
@@ -823,9 +911,12 @@ struct Forward {
     // 32 steps on operands `o`, issuing the next chunk's operand reads (n, from buffer nb) one
     // quad ahead of each group of four steps; column N history stored by the owner lane (rows
     // past T skipped: the steps of a partial chunk past T compute on stale rows, harmlessly).
+    // OWN: this wave holds column N (the others have no column-N code); ROUTED: its rows go to
+    // the LDS ring cnl (the routed hand-off consumer stores nothing itself)
+    template <bool OWN, bool ROUTED = false>
     __device__ __forceinline__ static void reg_chunk(const RegOps& o, RegOps& n, const char* nb, int etq, int ebq,
                                                      float& cur, unsigned& w, bool owner, float* __restrict__ cn,
-                                                     int t0, int T) {
+                                                     int t0, int T, float* cnl = nullptr) {
         float hist[8];
 #pragma unroll
         for (int p = 0; p < kChunk / 4; ++p) {
@@ -840,7 +931,11 @@ struct Forward {
 #pragma unroll
             for (int j = 0; j < 4; ++j) hist[(4 * p + j) & 7] = nv[j];
             cur = nv[3];
-            if ((p & 1) && owner) {  // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7]
+            if (OWN && ROUTED && (p & 1) && owner) {
+                float4* d4 = reinterpret_cast<float4*>(cnl + 8 * (p >> 1));
+                d4[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
+                d4[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+            } else if (OWN && !ROUTED && (p & 1) && owner) {  // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7]
                 const int tb = t0 + 8 * (p >> 1);
                 if (tb + 8 <= T) {
                     float4* d4 = reinterpret_cast<float4*>(cn + tb);
@@ -987,9 +1082,26 @@ struct Forward {
         wait_vm();  // (no load outlives the wave)
     }
 
+    // Whether this part's hand-off consumer (wave 0) is routed (Split::sbits).
+    __device__ __forceinline__ static bool consumer_routed(const Split* sp) { return kReg && SP && sp->p > 0; }
+    // The routed consumer's bitmap words of chunk qd (its owning lanes, as it would store them)
+    // and, when it holds column N, the chunk's column-N rows.
+    __device__ static void store_routed(const SegDesc& d, const Split* sp, int qd, unsigned* __restrict__ bits,
+                                        float* __restrict__ cn) {
+        const int l = lane_id();
+        const Layout L = Layout::make(C, d.N, sp->lanes);
+        const int g = Geo::lane_of(sp->p * W, l);
+        if (l >= Geo::HL && g < L.G) bits[(int64_t)qd * sp->lanes + g] = sp->sbits[(qd & 1) * kWave + l];
+        int own_w, own_l;
+        Geo::owner(L.G - 1, own_w, own_l);
+        if (uniform(own_w) == sp->p * W && l < kChunk && qd * kChunk + l < d.T)
+            cn[qd * kChunk + l] = sp->scn[(qd & 1) * kChunk + l];
+    }
     __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* raw,
-                                      int nch, int tok0, bool col0, bool stage, bool x4) {
+                                      int nch, int tok0, bool col0, bool stage, bool x4, const Split* sp = nullptr,
+                                      unsigned* __restrict__ bits = nullptr, float* __restrict__ cn = nullptr) {
         const int T = d.T;
+        const bool store = !col0 && !stage && sp && consumer_routed(sp);  // the idle helper of a part > 0
         if constexpr (VS == 32) {
             if (stage && x4 && !col0) {
                 stager_regs(d, E, lds, nch);
@@ -1045,6 +1157,9 @@ struct Forward {
 #ifdef WX_PHASE_TIMING
             unsigned long long hw = h0;
 #endif
+            // chunk q - 2's routed stores (its DP waves wrote them before barrier q - 1; they
+            // rewrite those ring slots after barrier q); the last two chunks: the DP waves
+            if (store && q >= 2) store_routed(d, sp, q - 2, bits, cn);
             if (stage && q + 2 < nch) {
                 wait_all_but(q + 3, q + kRing);  // chunk q + 2's DMA landed (later ones may be in flight)
 #ifdef WX_PHASE_TIMING
@@ -2101,6 +2216,9 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
     __shared__ int sbuf_lds[3 * (W + H)];
     __shared__ ColMapLds<VS> cml;
+    __shared__ unsigned sbits_lds[SP && C == 1 ? 2 * kWave : 1];  // Split::sbits
+    __shared__ __attribute__((aligned(16))) float scn_lds[SP && C == 1 ? 2 * kChunk : 1];
+    __shared__ uint64_t xring_lds[SP && C == 1 ? 3 * 32 : 1];
     const int P = SP ? a.parts : 1;
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
     // b % 8 — one XCD under the observed round-robin dispatch — and read its emission rows
@@ -2143,6 +2261,9 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         uint64_t* xseg = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
         sp.xin = xseg + (part > 0 ? part - 1 : 0) * kHaloCells;
         sp.xout = xseg + part * kHaloCells;
+        sp.sbits = sbits_lds;
+        sp.scn = scn_lds;
+        sp.xring = xring_lds;
     }
     if (SP && lane == 0) tsb[2] = 0;
     bool lost = false;

@@ -10,8 +10,10 @@
 // (profiles/r3_vad1h_kernel_stats.csv).  Here one workgroup per window:
 //   phase 1: pooled[t, c] = max over rows 3t .. 3t+2 of (|)x(|) -> written time-major, with
 //            per-channel fp64 sums and sums of squares;
-//   phase 2: mean / biased variance per channel (InstanceNorm1d, eps), the affine folded into
-//            one scale and shift, then y = leaky_relu(pooled * scale + shift) in place.
+//   phase 2: mean / biased variance per channel (InstanceNorm1d, eps), then
+//            y = leaky_relu((pooled - mean) * (rstd * gamma) + beta) in place (the centring
+//            first, as InstanceNorm1d: folding the mean into the shift loses the digits of a
+//            near-constant channel).
 // HBM: one read of x, one write + one read + one write of the pooled third.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
         }
     }
     __shared__ double red[kThreads / 4][8];  // (R <= kThreads / 4 when G >= 4)
-    __shared__ float coef[2][kMaxC];
+    __shared__ float coef[3][kMaxC];  // rstd * gamma, mean, beta
     // channel sums: row r's partials per group, then one thread per channel adds them in row order
     __shared__ double part[2][kMaxC];
     for (int rr = 0; rr < R; ++rr) {
@@ -88,7 +90,8 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
         const double rstd = 1.0 / sqrt(var + (double)a.eps);
         const double gm = a.gamma ? (double)a.gamma[tid] : 1.0, bt = a.beta ? (double)a.beta[tid] : 0.0;
         coef[0][tid] = (float)(rstd * gm);
-        coef[1][tid] = (float)(bt - mean * rstd * gm);
+        coef[1][tid] = (float)mean;
+        coef[2][tid] = (float)bt;
     }
     // this thread's pooled writes are re-read by this thread only; the barrier orders coef
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -96,14 +99,15 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     if (!active) return;
     const float4 sc = make_float4(coef[0][4 * g], coef[0][4 * g + 1], coef[0][4 * g + 2], coef[0][4 * g + 3]);
-    const float4 sh = make_float4(coef[1][4 * g], coef[1][4 * g + 1], coef[1][4 * g + 2], coef[1][4 * g + 3]);
+    const float4 mu = make_float4(coef[1][4 * g], coef[1][4 * g + 1], coef[1][4 * g + 2], coef[1][4 * g + 3]);
+    const float4 sh = make_float4(coef[2][4 * g], coef[2][4 * g + 1], coef[2][4 * g + 2], coef[2][4 * g + 3]);
     const float sl = a.slope;
     auto lrelu = [sl](float v) { return v > 0.0f ? v : v * sl; };
     for (int t = r; t < a.Lp; t += R) {
         float4* d = reinterpret_cast<float4*>(y + (int64_t)t * a.C) + g;
         const float4 p = *d;
-        *d = make_float4(lrelu(p.x * sc.x + sh.x), lrelu(p.y * sc.y + sh.y), lrelu(p.z * sc.z + sh.z),
-                         lrelu(p.w * sc.w + sh.w));
+        *d = make_float4(lrelu((p.x - mu.x) * sc.x + sh.x), lrelu((p.y - mu.y) * sc.y + sh.y),
+                         lrelu((p.z - mu.z) * sc.z + sh.z), lrelu((p.w - mu.w) * sc.w + sh.w));
     }
 }
 
@@ -113,13 +117,13 @@ extern "C" int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C,
                                 int32_t do_abs, const float* gamma, const float* beta, float eps, float slope,
                                 float* y, void* stream) {
     using namespace wxv;
-    if (B < 0 || L < 0 || C <= 0 || C > kMaxC || (C & 3) || x_window_stride < L * (int64_t)C || !x || !y)
-        return WX_E_INVALID;
-    if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 15) || (x_window_stride & 3))
-        return WX_E_INVALID;
+    if (B < 0 || L < 0 || C <= 0 || C > kMaxC || (C & 3) || x_window_stride < L * (int64_t)C) return WX_E_INVALID;
     if (L / 3 > 0x7fffffff || B > 0x7fffffff) return WX_E_INVALID;
     const int Lp = (int)(L / 3);
-    if (B == 0 || Lp == 0) return WX_OK;
+    if (B == 0 || Lp == 0) return WX_OK;  // (an empty output may have no storage)
+    if (!x || !y || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 15) ||
+        (x_window_stride & 3))
+        return WX_E_INVALID;
     SincArgs a;
     a.x = x;
     a.xb = x_window_stride;
