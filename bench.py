@@ -35,6 +35,8 @@ if ROOT not in sys.path:
 from whisperx_amd.synthetic import W2V_VOCAB  # noqa: E402  (no GPU touched at import)
 FRAME_S = 0.02  # wav2vec2 frame hop (320 samples at 16 kHz)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+STEP_CYCLES = 20  # one register-resident DP step: 5 dependent-chain VALU instructions x 4 cycles (wave64)
+ENGINE_PEAK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def log(*a):
@@ -716,6 +718,15 @@ def main():
                          "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6},
         }
         out["roofline"]["dp"] = _lib.status_summary(plan.status[: batch.S])
+        # The latency roofline: a segment's T steps are a dependent chain, and one step of the
+        # register-resident forward is 5 VALU instructions of one wave64 (4 cycles each: add,
+        # DPP add, compare, max3, add-with-carry; tools/ubench/step*.hip measures ~20 cycles
+        # alone), so no launch can beat T x 20 cycles at the 2.4 GHz peak engine clock.
+        t_max = int(max(batch.Ts))
+        floor_us = t_max * STEP_CYCLES / ENGINE_PEAK_GHZ / 1e3
+        out["roofline"]["latency"] = {"bound": "dependent DP steps", "T": t_max, "cycles_per_step": STEP_CYCLES,
+                                      "clock_GHz": ENGINE_PEAK_GHZ, "floor_us": floor_us,
+                                      "achieved_us": launch_s * 1e6, "frac": floor_us / (launch_s * 1e6)}
         mae, ntok, nbad = mae_vs_oracle([e.cpu().numpy() for e in ems], toks, plan)
         out["mae_ms"] = mae
         out["mae_detail"] = {"tokens": ntok, "segments_with_path_mismatch": nbad, "vs": "CPU oracle, same emission"}

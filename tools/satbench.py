@@ -24,6 +24,9 @@ CASES = {  # name: (segments, T, N range)
     "b32": (32, 1499, (300, 500)),
     "b128": (128, 1499, (300, 500)),
     "b64n900": (64, 2999, (850, 951)),
+    "b64p3": (64, 1499, (300, 400)),   # three parts per segment (column N in part 2)
+    "b64p4": (64, 1499, (430, 530)),   # four parts
+    "b64p2": (64, 1499, (170, 280)),   # two parts
     "sat1499": (4096, 1499, (300, 500)),
     "sat3000": (2048, 2999, (850, 951)),
     "sat3000_1024": (1024, 2999, (850, 951)),

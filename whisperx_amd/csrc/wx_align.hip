@@ -74,6 +74,44 @@ __device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
     return r;
 }
 
+// w <- 2w + sign(s - c): the same bit as shift_in wherever s and c are not both infinite
+// with one sign (inf - inf = NaN, whose sign bit is arbitrary) and not (-0, +0): in a
+// segment whose emission rows so far are all finite, every cell a backtrack path reads
+// (DESIGN.md §4.1).  Two VALU instructions with no VCC round trip.
+// Fused with the cell's maximum (one asm block per cell, so that hipcc cannot hoist the
+// eight cells' differences ahead of their uses: +14 VGPRs, a wave per SIMD lost).
+#ifndef WX_OPTFORM
+#define WX_OPTFORM 0
+#endif
+__device__ __forceinline__ void shift_sign_max(unsigned& w, float& cur, float c, float s) {
+#if WX_OPTFORM == 5  // (control: the comparison form itself)
+    w = shift_in(w, c, s);
+    cur = nan_max(s, c);
+#elif WX_OPTFORM == 4  // sign bit in one asm block, the maximum scheduled by hipcc
+    float d;
+    asm("v_sub_f32 %0, %2, %3\n\tv_alignbit_b32 %1, %1, %0, 31" : "=&v"(d), "+v"(w) : "v"(s), "v"(c));
+    cur = nan_max(s, c);
+#elif WX_OPTFORM == 3  // sign bit, scheduled by hipcc
+    w = __builtin_amdgcn_alignbit(w, __builtin_bit_cast(unsigned, s - c), 31);
+    cur = nan_max(s, c);
+#elif WX_OPTFORM == 1  // comparison + add-with-carry, maxNum
+    asm("v_cmp_gt_f32 vcc, %2, %3\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\tv_max_f32 %1, %3, %2"
+        : "+v"(w), "=v"(cur)
+        : "v"(c), "v"(s)
+        : "vcc");
+#elif WX_OPTFORM == 2  // sign bit, maxNum
+    float d;
+    asm("v_sub_f32 %0, %3, %4\n\tv_alignbit_b32 %1, %1, %0, 31\n\tv_max_f32 %2, %3, %4"
+        : "=&v"(d), "+v"(w), "=v"(cur)
+        : "v"(s), "v"(c));
+#else
+    float d;
+    asm("v_sub_f32 %0, %3, %4\n\tv_alignbit_b32 %1, %1, %0, 31\n\tv_maximum3_f32 %2, %3, %4, %4"
+        : "=&v"(d), "+v"(w), "=v"(cur)
+        : "v"(s), "v"(c));
+#endif
+}
+
 // Correctly rounded fp32 exp (the reference's torch-CPU exp is within 1 ULP of it).
 __device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
 
@@ -397,6 +435,10 @@ __device__ unsigned long long wx_cq[8192 * 48 * 3];
 // ahead.  Each part then arrives at a per-segment counter;
 // the last to arrive runs the argmax, the walk and merge_repeats.
 constexpr int kMaxParts = 4;
+// Column-N history: segment s at (row0 + kCnPad s) rounded down to 16 bytes, so at least
+// kCnPad - 3 floats past its T rows are its own: the register-resident owner stores all four
+// 8-row groups of a partial last chunk, up to 31 rows past T.
+constexpr int kCnPad = 40;
 constexpr int kXcdStride = 8;  // blocks b and b + 8 share an XCD (MI355X: 8 XCDs, round-robin)
 __host__ __device__ constexpr unsigned split_grid(int S, int P) {
     return (unsigned)((S + kXcdStride - 1) / kXcdStride * kXcdStride * P);
@@ -413,16 +455,13 @@ struct Split {
     uint64_t* xout;   // granules to part p+1 (p < P-1)
     int xstride;      // granules per chunk block of one segment boundary
     int spin;         // re-reads before a hand-off counts as lost (kMaxSpin; 0 in the recovery test)
-    // The hand-off consumer (wave 0) of a part > 0 of a register-resident kernel, unless it
-    // holds column N: it leaves its bitmap words in an LDS ring (two chunks) for the idle
-    // helper wave to store, so its only vector-memory operations in flight are the granule
-    // prefetches — issued two chunks ahead by LDS-DMA into a ring of three chunk slots (32
-    // granules each) and waited for with a hand-counted vmcnt.  (hipcc's own waits could not do
-    // this: with loads and stores both pending it waits vmcnt(0), which paid the prefetch
-    // issued a chunk earlier and the previous chunk's store round trip at every chunk.)
-    unsigned* sbits;  // LDS [2][64]
-    float* scn;       // LDS [2][32]: its column-N rows when the consumer also holds column N
-    uint64_t* xring;  // LDS [3][32]
+    // Register-resident kernels: the idle helper wave of a part > 0 polls the granules of
+    // chunk q and leaves their values in xg[q & 1] before barrier q; the hand-off consumer (DP
+    // wave 0) reads them there after the barrier like any other wave's halo, so no DP wave
+    // issues a global load.  (Routed through the consumer itself — prefetches two chunks ahead
+    // by LDS-DMA, hand-counted vmcnt, its bitmap stores handed to the helper — every missed
+    // prefetch cost a round trip inside the chain and the parts drifted apart: 59.7 us.)
+    float* xg;  // LDS [2][32]
 };
 
 __device__ __forceinline__ void granule_store(uint64_t* g, float v, unsigned tag) {
@@ -478,6 +517,20 @@ struct Forward {
     // LDS read, no wait.  Micro-benchmarks (tools/ubench/step*.hip): a step costs ~20 cycles
     // of one wave alone, each LDS read issued inside the chain ~9 more.
     static constexpr bool kReg = C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS;
+    // Cell pairs through v_pk_add_f32 (the throughput buckets, C even)
+#ifndef WX_PACKED
+    static constexpr bool kPackedAdds = false;
+#else
+    static constexpr bool kPackedAdds = C >= 4 && C % 2 == 0 && MODE == 0;
+#endif
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    // Sign-bit decisions (shift_sign) in the throughput buckets, per chunk while the
+    // segment's emission rows have all been finite (sticky: Forward::rows_finite)
+#ifndef WX_SIGNBITS
+    static constexpr bool kSignBits = false;
+#else
+    static constexpr bool kSignBits = MODE == 0 && !H && !SP && VS != kGatherVS;
+#endif
     static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
     static constexpr int kQS = quad_stride<VS>();
 
@@ -529,6 +582,9 @@ struct Forward {
     }
 
     // All waves of the workgroup call run(); with H, wave W is the helper.
+    // OPT (kSignBits): the decision bits by shift_sign_max while every staged row has been
+    // finite; returns true when one was not (the caller then runs the comparison form).
+    template <bool OPT = false>
     __device__ __forceinline__ static bool run(const SegDesc& d, const float* __restrict__ E, int V,
                                                const int32_t* __restrict__ tok,
                                                unsigned* __restrict__ bits,  // MODE 0: segment's bitmap
@@ -553,7 +609,7 @@ struct Forward {
             if constexpr (kReg) {
                 int t0 = N > 0 ? tok[d.tok0] : 0;
                 t0 = (t0 >= 0 && t0 < V) ? t0 : 0;
-                helper_reg(d, E, V, lds, lds + kBufs * kBufFloats, nch, t0, col0, wv == W, x4, sp, bits, cn);
+                return helper_reg(d, E, V, lds, lds + kBufs * kBufFloats, nch, t0, col0, wv == W, x4, sp);
             } else {
                 helper(d, E, V, lds, c0b, nch, x4, cm, col0, NH == 1 || wv == W);
             }
@@ -586,7 +642,6 @@ struct Forward {
         const bool xpub = SP && wv == W - 1 && sp->p + 1 < sp->P && Geo::lane_of(vw + 1, Geo::HL) < L.G;
         const bool xsub = SP && wv == 0 && sp->p > 0;
         // (own_w, own_l below: column N's wave and lane)
-        bool route = false;
         const int f = L.first(g), cnt = L.count(g);
         const bool is_short = g < L.n_short;
         // per-slot LDS byte offsets of em[., tok[j-1]]
@@ -604,7 +659,6 @@ struct Forward {
         Geo::owner(L.G - 1, own_w, own_l);
         const bool owner = uniform(own_w) == vw && l == own_l;
         const bool owner_wave = uniform(own_w) == vw;
-        route = kReg && xsub;
 
         State st;
         if (MODE == 1) {
@@ -637,13 +691,14 @@ struct Forward {
         // own registers (a loop-carried swap would make hipcc wait for both loads).
         uint64_t xodd[C], xeven[C];
         bool xlost = false;  // SP: a hand-off timed out
+        bool clean = true;   // OPT: every emission row staged so far is finite
 #pragma unroll
         for (int k = 0; k < C; ++k) xodd[k] = xeven[k] = 0;
         // Prefetches are issued by every lane, unconditionally (chunk and lane clamped into the
         // segment's granule block): a lane- or chunk-conditional load merges into the old
         // value's register, and hipcc then waits for the load right where it is issued.
         const int xl = min(l, Geo::HL - 1) * C;
-        if (SP && xsub && !route) {
+        if (SP && xsub && !kReg) {
 #pragma unroll
             for (int k = 0; k < C; ++k) {
                 xodd[k] = granule_load(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride + xl + k);
@@ -668,12 +723,10 @@ struct Forward {
         const int etq = (vw == 0 && l == 0) ? VS * 16 : toff[0] * 4;  // quad byte offset of this lane's column
         const int ebq = boff * 4;                                      // ... of the blank (uniform)
         if (kReg) __syncthreads();  // barrier -1 (helper_reg: the column-0 helper's first two chunks)
-        // XS (compile time): the routed hand-off consumer (Split::sbits): no global store in its
-        // code path.  OWN: the wave holding column N (the only one with column-N stores; the
+        // OWN (compile time): the wave holding column N (the only one with column-N stores; the
         // others have no branch around them: a taken branch per eight steps cost the DP waves
         // ~20% of their step time).
-        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C], RegOps& o, RegOps& n, auto xs, auto own) {
-            constexpr bool XS = decltype(xs)::value;
+        auto chunk_iter = [&](const int q, uint64_t(&xpre)[C], RegOps& o, RegOps& n, auto own) {
             constexpr bool OWN = decltype(own)::value;
             WX_T(c0);
             float* buf = lds + (q % kBufs) * kBufFloats;
@@ -683,12 +736,10 @@ struct Forward {
 #pragma unroll
                 for (int k = 0; k < C; ++k) xq[wv * kWave + (l - (kWave - Geo::HL)) * C + k] = st.cur[k];
             }
-            if constexpr (!XS) {
-                if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
-                    uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
+            if (SP && xpub && q > 0 && l >= kWave - Geo::HL) {  // ... and to the next part (row 32q)
+                uint64_t* go = sp->xout + (int64_t)q * sp->xstride + (l - (kWave - Geo::HL)) * C;
 #pragma unroll
-                    for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
-                }
+                for (int k = 0; k < C; ++k) granule_store(go + k, st.cur[k], sp->tag);
             }
             if (SP && xpub) WX_CQ(q, 1);
             WX_T(c1);
@@ -703,13 +754,9 @@ struct Forward {
 #pragma unroll
                 for (int k = 0; k < C; ++k) st.cur[k] = xq[(wv - 1) * kWave + l * C + k];
             }
-            if constexpr (XS) {  // chunk q's DMA landed (chunk q + 1's may be in flight)
-                if (q > 0) {
-                    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                    xpre[0] = sp->xring[(q % 3) * 32 + min(l, Geo::HL - 1)];
-                }
-            }
-            if (SP && xsub && q > 0) {
+            if (kReg && SP && xsub && q > 0) {  // (the poller's values: Split::xg)
+                if (l < Geo::HL) st.cur[0] = sp->xg[(q & 1) * 32 + l];
+            } else if (SP && xsub && q > 0) {
                 // Halo of row 32q from the previous part: the granules prefetched two chunks
                 // ago (the sc1 load takes longer than a chunk).  A part must trail its
                 // predecessor by more than the prefetch distance plus the hand-off latency for
@@ -740,19 +787,11 @@ struct Forward {
 #endif
                 // this set's next chunk, q + 2 (the old values are dead: keep the load below)
                 __builtin_amdgcn_sched_barrier(0);
-                if constexpr (XS) {
-                    if (l < 16)  // 32 granules = 16 lanes x 16 bytes into ring slot (q + 2) % 3
-                        glds_dwordx4_sc1(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride, (unsigned)l * 16u,
-                                         (unsigned)uniform((int)lds_addr(sp->xring + ((q + 2) % 3) * 32)));
-                } else {
 #pragma unroll
-                    for (int k = 0; k < C; ++k)
-                        xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
-                }
+                for (int k = 0; k < C; ++k)
+                    xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
             }
-            if constexpr (!XS) {
-                if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
-            }
+            if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
@@ -767,8 +806,7 @@ struct Forward {
                 // the next chunk's operands (the last chunk re-reads its own rows: harmless)
                 const char* nb = reinterpret_cast<const char*>(lds + ((q + 1 < nch ? q + 1 : q) % kBufs) * kBufFloats);
                 float cur0 = st.cur[0];
-                reg_chunk<OWN, XS>(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T,
-                                   XS ? sp->scn + (q & 1) * kChunk : nullptr);
+                reg_chunk<OWN>(o, n, nb, etq, ebq, cur0, st.w[0], owner, cn, q * kChunk, T);
                 // Invariant: on a partial last chunk reg_chunk runs all 32 steps on stale rows,
                 // so st.cur then holds the cell 32 steps on, not `rows` steps: nothing reads the
                 // state after the last chunk (its bits are masked below, column N stops at T).
@@ -776,11 +814,19 @@ struct Forward {
                 // hist[(rows - 1) & 7] instead.
                 st.cur[0] = cur0;
                 st.t += rows;
-            } else if (vw == 0) {
-                (void)OWN;
-                chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             } else {
-                chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                (void)OWN;
+                if constexpr (OPT) clean = clean && rows_finite(buf, rows, V);
+                if constexpr (OPT) {
+                    if (vw == 0)
+                        chunk<true, true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                    else
+                        chunk<false, true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                } else if (vw == 0) {
+                    chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                } else {
+                    chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                }
             }
             WX_T(c4);
 #ifdef WX_PHASE_TIMING
@@ -796,9 +842,7 @@ struct Forward {
                     // step, the bits of the steps past T are dropped)
                     const unsigned wq = kReg ? (st.w[k] & (0xFFFFFFFFu << sh))
                                              : ((sh == 0) ? st.w[k] : (st.w[k] << sh));
-                    if (XS)
-                        sp->sbits[(q & 1) * kWave + l] = wq;  // (C == 1)
-                    else if (SP)
+                    if (SP)
                         wdef[k] = wq;
                     else if (!halo && g < L.G)  // (lanes past column N: words the walk never reads)
                         bits[((int64_t)q * C + k) * lanes + g] = wq;
@@ -807,40 +851,19 @@ struct Forward {
             }
         };
         if constexpr (SP) {
-            auto loop = [&](auto xs, auto own) {
+            auto loop = [&](auto own) {
                 for (int q = 0; q < nch; q += 2) {
-                    chunk_iter(q, xeven, opsA, opsB, xs, own);
-                    if (q + 1 < nch) chunk_iter(q + 1, xodd, opsB, opsA, xs, own);
+                    chunk_iter(q, xeven, opsA, opsB, own);
+                    if (q + 1 < nch) chunk_iter(q + 1, xodd, opsB, opsA, own);
                 }
             };
-            if (route) {
-                // the first two chunks' granules (the plain-load path prefetches them below)
-                if (l < 16) {
-                    const unsigned base = (unsigned)uniform((int)lds_addr(sp->xring));
-                    glds_dwordx4_sc1(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride, (unsigned)l * 16u, base + 32u * 8u);
-                    glds_dwordx4_sc1(sp->xin + (int64_t)min(2, nch - 1) * sp->xstride, (unsigned)l * 16u, base + 64u * 8u);
-                }
-                if (owner_wave)
-                    loop(BoolTag<kReg>{}, BoolTag<true>{});
-                else
-                    loop(BoolTag<kReg>{}, BoolTag<false>{});
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA outlives the loop)
-                // the last two chunks' bitmap words and column-N rows (the helper stored up to
-                // chunk nch - 3)
-                for (int qd = max(nch - 2, 0); qd < nch; ++qd) {
-                    if (!halo && g < L.G) bits[(int64_t)qd * lanes + g] = sp->sbits[(qd & 1) * kWave + l];
-                    if (owner_wave && l < kChunk && qd * kChunk + l < T) cn[qd * kChunk + l] = sp->scn[(qd & 1) * kChunk + l];
-                }
-            } else if (owner_wave) {
-                loop(BoolTag<false>{}, BoolTag<true>{});
-            } else {
-                loop(BoolTag<false>{}, BoolTag<false>{});
-            }
-            if (!route && MODE == 0 && nch > 0 && !halo && g < L.G) {
-                store_deferred(nch - 1);
-            }
+            if (owner_wave)
+                loop(BoolTag<true>{});
+            else
+                loop(BoolTag<false>{});
+            if (MODE == 0 && nch > 0 && !halo && g < L.G) store_deferred(nch - 1);
         } else {
-            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB, BoolTag<false>{}, BoolTag<true>{});
+            for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB, BoolTag<true>{});
         }
 #ifdef WX_PHASE_TIMING
         if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
@@ -856,7 +879,7 @@ struct Forward {
             }
         }
 #endif
-        return xlost;
+        return xlost || !clean;
     }
 
     // ---------------------------------------------------------------- register-resident chunks
@@ -911,12 +934,11 @@ struct Forward {
     // 32 steps on operands `o`, issuing the next chunk's operand reads (n, from buffer nb) one
     // quad ahead of each group of four steps; column N history stored by the owner lane (rows
     // past T skipped: the steps of a partial chunk past T compute on stale rows, harmlessly).
-    // OWN: this wave holds column N (the others have no column-N code); ROUTED: its rows go to
-    // the LDS ring cnl (the routed hand-off consumer stores nothing itself)
-    template <bool OWN, bool ROUTED = false>
+    // OWN: this wave holds column N (the others have no column-N code)
+    template <bool OWN>
     __device__ __forceinline__ static void reg_chunk(const RegOps& o, RegOps& n, const char* nb, int etq, int ebq,
                                                      float& cur, unsigned& w, bool owner, float* __restrict__ cn,
-                                                     int t0, int T, float* cnl = nullptr) {
+                                                     int t0, int T) {
         float hist[8];
 #pragma unroll
         for (int p = 0; p < kChunk / 4; ++p) {
@@ -931,21 +953,14 @@ struct Forward {
 #pragma unroll
             for (int j = 0; j < 4; ++j) hist[(4 * p + j) & 7] = nv[j];
             cur = nv[3];
-            if (OWN && ROUTED && (p & 1) && owner) {
-                float4* d4 = reinterpret_cast<float4*>(cnl + 8 * (p >> 1));
+            if (OWN && (p & 1) && owner) {
+                // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7], whole groups: rows past T land in
+                // the segment's padding (kCnPad).  (A partial-group path here cost a taken
+                // branch per 8 steps in the wave that paces its part: 55.7 -> 51 us.)
+                const int tb = t0 + 8 * (p >> 1);
+                float4* d4 = reinterpret_cast<float4*>(cn + tb);
                 d4[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
                 d4[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
-            } else if (OWN && !ROUTED && (p & 1) && owner) {  // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7]
-                const int tb = t0 + 8 * (p >> 1);
-                if (tb + 8 <= T) {
-                    float4* d4 = reinterpret_cast<float4*>(cn + tb);
-                    d4[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
-                    d4[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k)
-                        if (tb + k < T) cn[tb + k] = hist[k];
-                }
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -1082,30 +1097,37 @@ struct Forward {
         wait_vm();  // (no load outlives the wave)
     }
 
-    // Whether this part's hand-off consumer (wave 0) is routed (Split::sbits).
-    __device__ __forceinline__ static bool consumer_routed(const Split* sp) { return kReg && SP && sp->p > 0; }
-    // The routed consumer's bitmap words of chunk qd (its owning lanes, as it would store them)
-    // and, when it holds column N, the chunk's column-N rows.
-    __device__ static void store_routed(const SegDesc& d, const Split* sp, int qd, unsigned* __restrict__ bits,
-                                        float* __restrict__ cn) {
+    // The idle helper of a part > 0 (register-resident kernels): chunk q's halo granules from
+    // part p - 1 into Split::xg[q & 1], re-reading until every tag matches (bounded: returns
+    // whether the hand-off was lost).  Only loads in this wave.  `pre` holds chunk q's first
+    // read, issued before barrier q - 1 (so a part that trails its predecessor finds the
+    // granules without a round trip inside its chunk); chunk q + 1's is issued on the way out.
+    __device__ static bool poll_halo(const Split* sp, int q, int nch, bool lost, uint64_t& pre) {
+        constexpr int HL = Geo::HL;
         const int l = lane_id();
-        const Layout L = Layout::make(C, d.N, sp->lanes);
-        const int g = Geo::lane_of(sp->p * W, l);
-        if (l >= Geo::HL && g < L.G) bits[(int64_t)qd * sp->lanes + g] = sp->sbits[(qd & 1) * kWave + l];
-        int own_w, own_l;
-        Geo::owner(L.G - 1, own_w, own_l);
-        if (uniform(own_w) == sp->p * W && l < kChunk && qd * kChunk + l < d.T)
-            cn[qd * kChunk + l] = sp->scn[(qd & 1) * kChunk + l];
+        const uint64_t* gi = sp->xin + (int64_t)q * sp->xstride + min(l, HL - 1) * C;
+        uint64_t x = pre;
+        bool ok = l >= HL || (unsigned)(x >> 32) == sp->tag;
+        for (int it = 0; !lost && !__all(ok) && it < sp->spin; ++it) {
+            x = granule_load(gi);
+            ok = l >= HL || (unsigned)(x >> 32) == sp->tag;
+        }
+        if (l < HL) sp->xg[(q & 1) * 32 + l] = __builtin_bit_cast(float, (unsigned)x);
+        pre = granule_load(gi + (int64_t)(min(q + 1, nch - 1) - q) * sp->xstride);
+        return !__all(ok);
     }
-    __device__ static void helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* raw,
-                                      int nch, int tok0, bool col0, bool stage, bool x4, const Split* sp = nullptr,
-                                      unsigned* __restrict__ bits = nullptr, float* __restrict__ cn = nullptr) {
+    __device__ static bool helper_reg(const SegDesc& d, const float* __restrict__ E, int V, float* lds, float* raw,
+                                      int nch, int tok0, bool col0, bool stage, bool x4, const Split* sp = nullptr) {
         const int T = d.T;
-        const bool store = !col0 && !stage && sp && consumer_routed(sp);  // the idle helper of a part > 0
+        // the idle helper of a part > 0 that holds columns (the previous part publishes nothing
+        // for a part without any)
+        const bool poll = SP && !col0 && !stage && sp && sp->p > 0 &&
+                          Geo::lane_of(sp->p * W, Geo::HL) < Layout::make(C, d.N, sp->lanes).G;
+        bool lost = false;
         if constexpr (VS == 32) {
             if (stage && x4 && !col0) {
                 stager_regs(d, E, lds, nch);
-                return;
+                return false;
             }
         }
         auto buf = [&](int q) { return lds + (q % kBufs) * kBufFloats; };
@@ -1141,6 +1163,8 @@ struct Forward {
             issue(kRing - 1);
         }
         double acc = 0.0;
+        uint64_t pre = 0;  // poll: chunk 1's granules (first read)
+        if (poll) pre = granule_load(sp->xin + (int64_t)min(1, nch - 1) * sp->xstride + min(lane_id(), Geo::HL - 1) * C);
         __syncthreads();  // barrier -1
         if (col0) {
             col0_pre(0, d, buf(0), tok0, acc);
@@ -1157,9 +1181,6 @@ struct Forward {
 #ifdef WX_PHASE_TIMING
             unsigned long long hw = h0;
 #endif
-            // chunk q - 2's routed stores (its DP waves wrote them before barrier q - 1; they
-            // rewrite those ring slots after barrier q); the last two chunks: the DP waves
-            if (store && q >= 2) store_routed(d, sp, q - 2, bits, cn);
             if (stage && q + 2 < nch) {
                 wait_all_but(q + 3, q + kRing);  // chunk q + 2's DMA landed (later ones may be in flight)
 #ifdef WX_PHASE_TIMING
@@ -1168,6 +1189,12 @@ struct Forward {
                 transpose_quads(ring(q + 2), buf(q + 2));
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads done: the slot is free
                 issue(q + kRing);
+            }
+            if (poll && q > 0) {
+                lost = poll_halo(sp, q, nch, lost, pre) || lost;
+#ifdef WX_PHASE_TIMING
+                hw = __builtin_amdgcn_s_memtime();  // (the poll counts as the DMA wait)
+#endif
             }
             WX_T(h1);
             __syncthreads();  // barrier q
@@ -1188,6 +1215,7 @@ struct Forward {
             o[2] = acc_vm;
         }
 #endif
+        return lost;
     }
 
     // The helper wave (H): mirrors the DP waves' barriers.  Before barrier q, chunks q and
@@ -1284,9 +1312,29 @@ struct Forward {
         }
     }
 
+    // Whether rows [0, rows) of a staged chunk buffer (row-major, VS floats a row) are finite in
+    // columns [0, V): lane l scans half a row (16-byte LDS reads), wave-uniform result.
+    __device__ __forceinline__ static bool rows_finite(const float* buf, int rows, int V) {
+        const int l = lane_id();
+        const int r = l >> 1, c0 = (l & 1) * (VS / 2);
+        float m = 0.0f;
+        if (r < rows) {
+#pragma unroll
+            for (int c = 0; c < VS / 2; c += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(buf + r * VS + c0 + c);
+                const int cc = c0 + c;
+                m = __builtin_elementwise_maximum(m, cc < V ? fabsf(v.x) : 0.0f);
+                m = __builtin_elementwise_maximum(m, cc + 1 < V ? fabsf(v.y) : 0.0f);
+                m = __builtin_elementwise_maximum(m, cc + 2 < V ? fabsf(v.z) : 0.0f);
+                m = __builtin_elementwise_maximum(m, cc + 3 < V ? fabsf(v.w) : 0.0f);
+            }
+        }
+        return __all(m < INFINITY);  // (NaN: false)
+    }
+
     // One chunk's steps: unrolled groups of kUnroll with immediate LDS row offsets, then the
     // remainder.  WAVE0: this wave holds column 1 (its left input is column 0).
-    template <bool WAVE0>
+    template <bool WAVE0, bool SG = false>
     __device__ __forceinline__ static void chunk(const char* bb, const float* c0q, int rows, const int (&toff)[C],
                                                  int boff, State& st, int inf_from, bool is_short, bool halo, int f,
                                                  int cnt, bool owner, int N, float* __restrict__ cn,
@@ -1294,13 +1342,13 @@ struct Forward {
         constexpr int kColLds = 3, kColFinite = 1, kColAny = 2;
         if (kPipelined && rows == kChunk) {  // software-pipelined full chunk
             if (!WAVE0)
-                pipelined_chunk<0>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<0, SG>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
             else if (H)
-                pipelined_chunk<kColLds>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColLds, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else if (st.t + kChunk < inf_from)
-                pipelined_chunk<kColFinite>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColFinite, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else
-                pipelined_chunk<kColAny>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColAny, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             return;
         }
         int r = 0;
@@ -1313,7 +1361,7 @@ struct Forward {
             if (!WAVE0 || H || st.t + kU < inf_from) {  // column 0 from LDS, or finite for the group
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
+                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite), SG>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
                                                                  inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
@@ -1321,7 +1369,7 @@ struct Forward {
             } else {
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    step<kColAny>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
+                    step<kColAny, SG>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
                 }
@@ -1338,7 +1386,7 @@ struct Forward {
             const char* ga[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-            step<!WAVE0 ? 0 : (H ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
+            step<!WAVE0 ? 0 : (H ? kColLds : kColAny), SG>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
                                                        cnt, N, tr);
             if (MODE == 0 && owner) cn[st.t] = st.cur[C - 1];
             ++st.t;
@@ -1349,7 +1397,7 @@ struct Forward {
     // computes.  sched_barrier keeps the scheduler from sinking the loads back to their uses
     // (it does, to minimise registers); the waitcnt pass counts them exactly, since LDS
     // returns in order.
-    template <int COL>
+    template <int COL, bool SG = false>
     __device__ __forceinline__ static void pipelined_chunk(const char* bb, const float* c0q, const int (&toff)[C],
                                                            int boff, State& st, int inf_from, bool is_short,
                                                            bool halo, int f, int cnt, bool owner, int N,
@@ -1390,7 +1438,7 @@ struct Forward {
                 c0_of(rw[u + 3], u + 3);
             }
             __builtin_amdgcn_sched_barrier(0);
-            advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
+            advance<COL, SG>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
             hist[u & (kUnroll - 1)] = st.cur[C - 1];
             ++st.t;
             if (MODE == 0 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
@@ -1404,13 +1452,13 @@ struct Forward {
     // One time step t -> t+1 (alignment.py:372-378).  COL: 0 = not the column-1 wave (lane
     // 0's left input is a halo edge, don't-care); column-1 wave: 1 = column 0 finite for the
     // next row, 2 = general column 0, 3 = column 0 read from the helper's LDS row.
-    template <int COL>
+    template <int COL, bool SG = false>
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 const float* c0, State& st, int inf_from, bool is_short, bool halo,
                                                 int f, int cnt, int N, float* __restrict__ tr) {
         Row rw;
         load_row<COL>(gb, ga, ro, boff, c0, rw);
-        advance<COL>(gb, ro, c0, rw, st, inf_from, is_short, halo, f, cnt, N, tr);
+        advance<COL, SG>(gb, ro, c0, rw, st, inf_from, is_short, halo, f, cnt, N, tr);
     }
 
     // The LDS operands of one step: em[t, blank], em[t, tok[j-1]] per slot, column 0 (COL 3).
@@ -1429,7 +1477,7 @@ struct Forward {
         if (COL == 1 || COL == 2) rw.c0 = *reinterpret_cast<const float*>(gb + ro);  // em[t, 0]
     }
 
-    template <int COL>
+    template <int COL, bool SG = false>
     __device__ __forceinline__ static void advance(const char* gb, int ro, const float* c0, const Row& rw, State& st,
                                                    int inf_from, bool is_short, bool halo, int f, int cnt, int N,
                                                    float* __restrict__ tr) {
@@ -1452,12 +1500,45 @@ struct Forward {
             left = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src), 0x138 /* wave_shr:1 */,
                                                                       0xF, 0xF, true));
         }
+        if constexpr (kPackedAdds) {
+            // the stay sums of cell pairs with v_pk_add_f32 (two IEEE fp32 adds per
+            // instruction, the same roundings; the blank operand broadcast).  (The change sums
+            // too — cells (2i+1, 2i+2) from the pair (2i, 2i+1) — cost a v_mov per pair to
+            // gather the two token operands into a register pair.)
+            float s[C], c[C];
 #pragma unroll
-        for (int k = C - 1; k >= 0; --k) {
-            const float s = st.cur[k] + eb;
-            const float c = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
-            if (MODE == 0) st.w[k] = shift_in(st.w[k], c, s);
-            st.cur[k] = nan_max(s, c);
+            for (int i = 0; i < C / 2; ++i) {
+                const f32x2 sp = f32x2{st.cur[2 * i], st.cur[2 * i + 1]} + f32x2{eb, eb};
+                s[2 * i] = sp.x;
+                s[2 * i + 1] = sp.y;
+            }
+#pragma unroll
+            for (int k = 0; k < C; ++k) c[k] = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
+#pragma unroll
+            for (int k = C - 1; k >= 0; --k) {
+                if (MODE == 0 && SG) {
+                    float v;
+                    shift_sign_max(st.w[k], v, c[k], s[k]);
+                    st.cur[k] = v;
+                } else {
+                    if (MODE == 0) st.w[k] = shift_in(st.w[k], c[k], s[k]);
+                    st.cur[k] = nan_max(s[k], c[k]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = C - 1; k >= 0; --k) {
+                const float s = st.cur[k] + eb;
+                const float c = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
+                if (MODE == 0 && SG) {
+                    float v;
+                    shift_sign_max(st.w[k], v, c, s);
+                    st.cur[k] = v;
+                } else {
+                    if (MODE == 0) st.w[k] = shift_in(st.w[k], c, s);
+                    st.cur[k] = nan_max(s, c);
+                }
+            }
         }
         if (COL == 1 || COL == 2) {
             const float e0 = rw.c0;
@@ -1929,7 +2010,10 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
 // Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
 // block, or -1), meaningful in wave 0.
 constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
-constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment
+#ifndef WX_SPEC_OVERLAP
+#define WX_SPEC_OVERLAP 2
+#endif
+constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker starts above its segment
 // wave 0's t_start search, in walk blocks (A/B: 1, 3 or 5 within noise)
 constexpr int kSpecArgmaxBlocks = 3;
 template <int CC>
@@ -2216,9 +2300,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
     __shared__ int sbuf_lds[3 * (W + H)];
     __shared__ ColMapLds<VS> cml;
-    __shared__ unsigned sbits_lds[SP && C == 1 ? 2 * kWave : 1];  // Split::sbits
-    __shared__ __attribute__((aligned(16))) float scn_lds[SP && C == 1 ? 2 * kChunk : 1];
-    __shared__ uint64_t xring_lds[SP && C == 1 ? 3 * 32 : 1];
+    __shared__ float xg_lds[SP && C == 1 ? 2 * 32 : 1];  // Split::xg
     const int P = SP ? a.parts : 1;
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
     // b % 8 — one XCD under the observed round-robin dispatch — and read its emission rows
@@ -2247,7 +2329,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     const float* E = a.em + d.row0 * a.V;
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
-    float* cn = a.cn + ((d.row0 + 4 * (int64_t)seg) & ~(int64_t)3);
+    float* cn = a.cn + ((d.row0 + kCnPad * (int64_t)seg) & ~(int64_t)3);
     WX_STAMP_RT(4);
     WX_STAMP(0);
     Split sp;
@@ -2261,17 +2343,28 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         uint64_t* xseg = a.xg + ((d.row0 >> 5) + seg) * (int64_t)sp.xstride;
         sp.xin = xseg + (part > 0 ? part - 1 : 0) * kHaloCells;
         sp.xout = xseg + part * kHaloCells;
-        sp.sbits = sbits_lds;
-        sp.scn = scn_lds;
-        sp.xring = xring_lds;
+        sp.xg = xg_lds;
     }
-    if (SP && lane == 0) tsb[2] = 0;
+    if (lane == 0) tsb[2] = 0;
     bool lost = false;
-    if (!slow)
-        lost = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
-                                                     a.x4 != 0, cm, nullptr, &sp);
+    using Fwd = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>;
+    if constexpr (Fwd::kSignBits) {
+        // sign-bit decisions first; a segment with a non-finite emission row is run again with
+        // the comparison form (both forms in one chunk loop cost 14 VGPRs: a wave per SIMD)
+        if (!slow) {
+            if (Fwd::template run<true>(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp))
+                tsb[2] = 1;
+            block_fence();
+            if (tsb[2]) {
+                block_fence();  // (every wave has read the flag)
+                Fwd::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp);
+            }
+        }
+    } else if (!slow) {
+        lost = Fwd::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp);
+    }
     WX_STAMP(1);
-    if (SP && lost) tsb[2] = 1;  // (any lane of wave 0)
+    if (SP && lost) tsb[2] = 1;  // (any lane of the consumer or, register-resident kernels, the poller)
     wait_vm();
     block_fence();
     bool failed = false;
@@ -2369,8 +2462,11 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     WX_STAMP_RT(5);
 }
 
+#ifndef WX_MINWAVES
+#define WX_MINWAVES 1
+#endif
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(!H && C == 8 ? WX_MINWAVES : 1, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
 }
@@ -3718,7 +3814,7 @@ int align_mode(int32_t S, int32_t mode) {
 size_t cmask_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T / kChunk + S + 1) * 4u, 256); }
 
 // column N history: segment s at (row0 + 4 s) & ~3 (16-byte aligned groups of 8 rows)
-size_t cn_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T + 4 * (int64_t)S + 16) * 4u, 256); }
+size_t cn_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T + kCnPad * (int64_t)S + 16) * 4u, 256); }
 
 // split hand-off granules: per (floor(row0/32) + seg + chunk) block, 3 boundaries x 40
 size_t xg_bytes(int32_t S, int64_t sum_T) {
