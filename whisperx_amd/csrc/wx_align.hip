@@ -939,7 +939,7 @@ struct Forward {
     __device__ __forceinline__ static void reg_chunk(const RegOps& o, RegOps& n, const char* nb, int etq, int ebq,
                                                      float& cur, unsigned& w, bool owner, float* __restrict__ cn,
                                                      int t0, int T) {
-        float hist[8];
+        float hist[OWN ? kChunk : 1];
 #pragma unroll
         for (int p = 0; p < kChunk / 4; ++p) {
             n.et[p] = *reinterpret_cast<const float4*>(nb + p * kQS * 4 + etq);
@@ -950,19 +950,24 @@ struct Forward {
                 reg_steps4<true>(cur, w, o.et[p], o.eb[p], nv);
             else
                 reg_steps4<false>(cur, w, o.et[p], o.eb[p], nv);
+            if constexpr (OWN) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) hist[(4 * p + j) & 7] = nv[j];
-            cur = nv[3];
-            if (OWN && (p & 1) && owner) {
-                // rows tb + 1 .. tb + 8 -> cn[tb .. tb + 7], whole groups: rows past T land in
-                // the segment's padding (kCnPad).  (A partial-group path here cost a taken
-                // branch per 8 steps in the wave that paces its part: 55.7 -> 51 us.)
-                const int tb = t0 + 8 * (p >> 1);
-                float4* d4 = reinterpret_cast<float4*>(cn + tb);
-                d4[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
-                d4[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+                for (int j = 0; j < 4; ++j) hist[4 * p + j] = nv[j];
             }
+            cur = nv[3];
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if (OWN && owner) {
+            // rows t0 + 1 .. t0 + 32 -> cn[t0 .. t0 + 31], once per chunk and whole: rows past T
+            // land in the segment's padding (kCnPad).  (Stored per 8 steps inside the chain,
+            // with a partial-group path, they cost the pacing wave a taken branch and an EXEC
+            // round trip per 8 steps: 59.7 -> 55.3 -> ... us.)
+            // (Written through with sc1 stores — so that the arrival's release would have no
+            // dirty line to write back — the 32 single stores cost more than the release.)
+            float4* d4 = reinterpret_cast<float4*>(cn + t0);
+#pragma unroll
+            for (int i = 0; i < kChunk / 4; ++i)
+                d4[i] = make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]);
         }
     }
     // tr[t][0] + em[t, tok[0]] for the rows of chunk q (the column-1 wave's lane-0 operand),
@@ -2370,12 +2375,16 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     bool failed = false;
     if (SP && !slow) {  // release this part's bits / column-N history; the last part to arrive goes on
         if (lane == 0) {
+#if !defined(WX_DEV_NOFENCE) && !defined(WX_DEV_NOREL)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
             wait_vm();
             const unsigned w = split_arrive(a.arrive + seg, a.epoch, tsb[2] != 0);
             tsb[0] = ((w & 0x7Fu) == (unsigned)P) ? 1 + (int)((w >> 7) & 1u) : 0;
             if (tsb[0]) {
+#if !defined(WX_DEV_NOFENCE) && !defined(WX_DEV_NOACQ)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
                 wait_vm();
                 // every part has arrived: leave the counter clean for the next launch
                 __hip_atomic_store(a.arrive + seg, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

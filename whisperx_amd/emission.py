@@ -71,6 +71,37 @@ def _weight(conv: torch.nn.Conv1d) -> torch.Tensor:
     return w
 
 
+def _version(t: torch.Tensor) -> int:
+    """t._version; -1 for an inference tensor (it has no version counter)."""
+    try:
+        return t._version
+    except RuntimeError:
+        return -1
+
+
+def _tap_weights(conv: torch.nn.Conv1d) -> torch.Tensor:
+    """The GEMM operands of _conv1d_gemm, contiguous and cached until the weight changes:
+    [k, Cin, Cout] (one [Cin, Cout] matrix per tap) for an ungrouped conv, [G, k, Cg, Cout/G]
+    for a grouped one.  (A permuted view of the weight has no unit stride, so every GEMM on
+    it made torch copy the operand first: 26 copy kernels per 30 s forward, ~5% of its time.)"""
+    # keyed on the module's parameters (a weight_norm'd conv's `weight` is recomputed from
+    # weight_g / weight_v by a hook — a new, possibly inference, tensor at every call)
+    key = tuple((t.data_ptr(), _version(t)) for t in conv.parameters())
+    cached = getattr(conv, "_wx_tap_cache", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    w = _weight(conv)
+    G = conv.groups
+    Cout, Cg, k = w.shape
+    with torch.no_grad():
+        if G == 1 and Cg > 1:
+            t = w.detach().permute(2, 1, 0).contiguous()
+        else:
+            t = w.detach().reshape(G, Cout // G, Cg, k).permute(0, 3, 2, 1).contiguous()
+    conv._wx_tap_cache = (key, t)
+    return t
+
+
 def materialize_weights(model: torch.nn.Module) -> None:
     """Evaluate every parametrised Conv1d weight of a prepared model on the current stream, so
     that streams which then wait on it read a finished tensor (see _weight)."""
@@ -79,7 +110,7 @@ def materialize_weights(model: torch.nn.Module) -> None:
     with torch.no_grad():
         for mod in model.modules():
             if isinstance(mod, torch.nn.Conv1d) and hasattr(mod, "_wx_orig_forward"):
-                _weight(mod)
+                _tap_weights(mod)
             if "_wx_qkv" in mod.__dict__ and next(mod.parameters()).is_cuda:
                 _qkv_weights(mod)
 
@@ -105,7 +136,7 @@ def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
         return out.transpose(1, 2)
     if G == 1 and Cin > 1:
         # y = sum_j x[j::s] @ W[:, :, j]^T  (strided row views, no patch copy)
-        wt = w.permute(2, 1, 0)  # [k, Cin, Cout]
+        wt = _tap_weights(conv)  # [k, Cin, Cout]
         for bi in range(B):
             xb = xt[bi]
             ob = out[bi]
@@ -122,7 +153,7 @@ def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
     # patches: Cin == 1, or grouped.  wg: [G, k, Cg, Coutg]
     Cg = Cin // G
     Cog = Cout // G
-    wg = w.reshape(G, Cog, Cg, k).permute(0, 3, 2, 1)
+    wg = _tap_weights(conv)  # [G, k, Cg, Cog]
     for bi in range(B):
         xb = xt[bi]  # [Lp, Cin] contiguous
         acc = torch.zeros((G, Lout, Cog), dtype=x.dtype, device=x.device)
@@ -334,6 +365,8 @@ def restore_model(model: torch.nn.Module) -> torch.nn.Module:
             del mod._wx_orig_forward
         if hasattr(mod, "_wx_w_cache"):
             del mod._wx_w_cache
+        if hasattr(mod, "_wx_tap_cache"):
+            del mod._wx_tap_cache
         mod.__dict__.pop("_wx_qkv", None)
     if "_wx_gemm_conv" in model.__dict__:
         del model._wx_gemm_conv
