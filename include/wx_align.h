@@ -228,6 +228,16 @@ int wx_attention_f32(const float* q, const float* k, const float* v, float* o, i
                      int32_t D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                      float scale, void* stream);
 
+/* wav2vec2 encoder layer's residual add + LayerNorm (alignment.py:226-233, the emission
+ * forward: `layer_norm(residual + x)` twice per layer): for each of `rows` rows of D floats
+ * (D in {256, 512, 768, 1024}; row strides a_stride / b_stride elements, multiples of 4; all
+ * pointers 16-byte aligned), s = a + b, y = (s - mean(s)) / sqrt(var(s) + eps) * gamma + beta
+ * (biased variance, fp32, two passes over the row in registers).  y is [rows][D] contiguous;
+ * sum_out (may be NULL) receives s in the same layout.  Equal to torch's add + LayerNorm to
+ * fp32 tolerance (torch uses Welford), not bit-identical. */
+int wx_add_layernorm(const float* a, const float* b, int64_t rows, int32_t D, int64_t a_stride, int64_t b_stride,
+                     const float* gamma, const float* beta, float eps, float* y, float* sum_out, void* stream);
+
 /* VAD producer (vad.py:198-240 -> pyannote SincNet): the epilogue of one SincNet stage on the
  * time-major conv output x [B windows][L][C] (window stride x_window_stride elements, row
  * stride C; C % 4 == 0, C <= 128, 16-byte aligned): y[b][t][c] = leaky_relu(InstanceNorm1d(

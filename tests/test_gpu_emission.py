@@ -38,6 +38,30 @@ def test_channel_norm_vs_torch_groupnorm(L, C, gelu):
     assert torch.equal(inplace, got)
 
 
+@pytest.mark.parametrize("shape", [(1, 1499, 768), (2, 97, 1024), (1, 1, 768), (3, 5, 256), (1, 0, 512)])
+def test_add_layernorm_vs_torch(shape):
+    """wx_add_layernorm against torch's fp32 `layer_norm(a + b)` (the encoder layer's residual
+    step; torch's Welford vs two passes here: fp32 tolerance), the sum output equal to a + b,
+    and a row-strided operand (a column slice of a wider buffer)."""
+    from whisperx_amd import _lib
+
+    torch.manual_seed(sum(shape))
+    D = shape[-1]
+    wide = torch.randn(*shape[:-1], D + 8, device="cuda") * 2 + 0.5
+    a = wide[..., 4:4 + D] if shape[1] else torch.randn(shape, device="cuda")
+    b = torch.randn(shape, device="cuda")
+    ln = torch.nn.LayerNorm(D).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(torch.randn(D) * 0.3 + 1)
+        ln.bias.copy_(torch.randn(D) * 0.1)
+        ref = ln(a + b)
+    y, s = _lib.add_layernorm(a, b, ln.weight, ln.bias, ln.eps, want_sum=True)
+    assert y.shape == tuple(shape) and y.is_contiguous()
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
+    assert torch.equal(s, a + b)
+    torch.testing.assert_close(_lib.add_layernorm(a, b, ln.weight, ln.bias, ln.eps), ref, rtol=2e-5, atol=2e-5)
+
+
 @pytest.mark.parametrize("B,H,T", [(1, 12, 1), (1, 12, 31), (1, 12, 33), (1, 12, 400), (1, 12, 1499), (2, 16, 97)])
 def test_attention_f32_vs_fp64(B, H, T):
     """wx_attention_f32 on transformers' q/k/v views of [B, T, H*64] projections against an

@@ -56,6 +56,28 @@ def make_batch(S, T, V, n_lo, n_hi, seed, device):
     return [em[s] for s in range(S)], toks
 
 
+def make_ragged(S, V, seed, device):
+    """S segments of T ~ U[100, 1499] frames, N ~ U[T/6, T/3] tokens (VAD-chunk-like shapes)."""
+    import numpy as np
+    import torch
+
+    rng = np.random.default_rng(seed)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    ems, toks = [], []
+    for _ in range(S):
+        T = int(rng.integers(100, 1500))
+        N = int(rng.integers(max(1, T // 6), max(2, T // 3)))
+        logits = torch.randn((T, V), generator=g, device=device)
+        logits[:, 0] += 6.0
+        tk = rng.integers(1, V, N)
+        fr = np.sort(rng.choice(np.arange(1, T - 1), N, replace=False))
+        logits[torch.from_numpy(fr).to(device), torch.from_numpy(tk).to(device)] += 12.0
+        ems.append(torch.log_softmax(logits, -1))
+        toks.append(tk.tolist())
+    return ems, toks
+
+
 def child(args):
     import numpy as np
     import torch
@@ -92,8 +114,12 @@ def child(args):
             del tr, b
             torch.cuda.empty_cache()
             continue
-        S, T, (lo, hi) = CASES[case]
-        ems, toks = make_batch(S, T, 32, lo, hi, 1234, dev)
+        if case.startswith("rag"):  # ragged: rag64, rag16
+            S = int(case[3:])
+            ems, toks = make_ragged(S, 32, 4321, dev)
+        else:
+            S, T, (lo, hi) = CASES[case]
+            ems, toks = make_batch(S, T, 32, lo, hi, 1234, dev)
         b = _lib.Batch(ems, toks, [0] * S, device=dev)
         del ems
         p = _lib.AlignPlan(b, mode=args.mode)

@@ -74,6 +74,7 @@ SIGNATURES = {
     "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
     "wx_channel_norm_workspace_bytes": (_sz, [_i32]),
     "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
+    "wx_add_layernorm": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
@@ -521,6 +522,26 @@ def channel_norm(x: torch.Tensor, gamma, beta, eps: float, gelu: bool, out: Opti
         _check(lib.wx_channel_norm(_ptr(x), L, C, _ptr(gamma), _ptr(beta), float(eps), int(bool(gelu)), _ptr(y),
                                    _ptr(ws), ws.numel(), ctypes.c_void_p(stream.cuda_stream)))
     return y
+
+
+def add_layernorm(a: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                  want_sum: bool = False):
+    """wx_add_layernorm: LayerNorm(a + b) over the last dim of fp32 device tensors of one shape
+    (last dim contiguous, rows at any stride the leading dims flatten to).  Returns y, or
+    (y, a + b) with want_sum."""
+    lib = load()
+    D = int(a.shape[-1])
+    if tuple(a.shape) != tuple(b.shape):
+        raise WXError(f"add_layernorm: shapes differ ({tuple(a.shape)}, {tuple(b.shape)})")
+    a2, b2 = a.reshape(-1, D), b.reshape(-1, D)
+    rows = int(a2.shape[0])
+    y = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+    s = torch.empty_like(y) if want_sum else None
+    with torch.cuda.device(a.device):
+        _check(lib.wx_add_layernorm(_ptr(a2), _ptr(b2), rows, D, int(a2.stride(0)) if rows else D,
+                                    int(b2.stride(0)) if rows else D, _ptr(gamma), _ptr(beta), float(eps), _ptr(y),
+                                    _ptr(s) if s is not None else None, _stream(a.device)))
+    return (y, s) if want_sum else y
 
 
 def attention_f32(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:

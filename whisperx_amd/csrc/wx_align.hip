@@ -2041,6 +2041,10 @@ __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, i
     sw.top = (T - 1) >> 5;
     sw.L = max((sw.top + 1 + kSpecArgmaxBlocks + K - 1) / K, 1);
     sw.L0 = max(sw.L - kSpecArgmaxBlocks, 1);
+    while (K > 1 && sw.lo(K - 2) == 0) --K;  // (segments past block 0 would be empty)
+    sw.K = K;
+    sw.sres = sbuf + K;
+    sw.send = sbuf + 2 * K;
     const int tref = T;
     if (wv == 0) t_start = column_argmax(cn, T);
     if (wv == 0) {

@@ -269,6 +269,55 @@ __global__ __launch_bounds__(64 * kAttnSplit) void attn_f32_kernel(AttnArgs a) {
     }
 }
 
+// Residual add + LayerNorm over rows of D floats (the wav2vec2 encoder layer's
+// `layer_norm(residual + x)`, twice per layer): one wave per row, the row in registers (D / 256
+// float4 per lane), mean and biased variance in fp32 from the registers (two passes, not
+// torch's Welford: equal to fp32 tolerance), y = (s - mean) * rstd * gamma + beta.  Optionally
+// also writes the sum s (the pre-norm residual stream of the stable-layer-norm layers).
+template <int NV>  // float4 per lane: D = 256 NV
+__global__ __launch_bounds__(256) void add_ln_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float eps, int64_t rows, int64_t sa, int64_t sb, int64_t sy,
+                                                      float* __restrict__ y, float* __restrict__ sum_out) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int l = threadIdx.x & 63;
+    constexpr int D = 256 * NV;
+    const float4* pa = reinterpret_cast<const float4*>(a + row * sa);
+    const float4* pb = reinterpret_cast<const float4*>(b + row * sb);
+    float4 v[NV];
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float4 x = pa[64 * i + l], z = pb[64 * i + l];
+        v[i] = make_float4(x.x + z.x, x.y + z.y, x.z + z.z, x.w + z.w);
+        acc += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    const float mean = acc / (float)D;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+        q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+    float4* py = reinterpret_cast<float4*>(y + row * sy);
+    float4* ps = sum_out ? reinterpret_cast<float4*>(sum_out + row * sy) : nullptr;
+    const float4* pg = reinterpret_cast<const float4*>(gamma);
+    const float4* pt = reinterpret_cast<const float4*>(beta);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const float4 g = pg[64 * i + l], t = pt[64 * i + l];
+        py[64 * i + l] = make_float4((v[i].x - mean) * rstd * g.x + t.x, (v[i].y - mean) * rstd * g.y + t.y,
+                                     (v[i].z - mean) * rstd * g.z + t.z, (v[i].w - mean) * rstd * g.w + t.w);
+        if (ps) ps[64 * i + l] = v[i];
+    }
+}
+
 }  // namespace wxe
 
 extern "C" size_t wx_channel_norm_workspace_bytes(int32_t C) {
@@ -329,6 +378,29 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     a.scale_log2 = scale * 1.4426950408889634f;
     hipLaunchKernelGGL(attn_f32_kernel, dim3((unsigned)((T + 31) / 32), (unsigned)(B * H)), dim3(64 * kAttnSplit), 0,
                        reinterpret_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_add_layernorm(const float* a, const float* b, int64_t rows, int32_t D, int64_t a_stride,
+                                int64_t b_stride, const float* gamma, const float* beta, float eps, float* y,
+                                float* sum_out, void* stream) {
+    using namespace wxe;
+    if (rows < 0 || (D != 768 && D != 1024 && D != 512 && D != 256)) return WX_E_INVALID;
+    if (rows == 0) return WX_OK;  // (an empty tensor may have no storage)
+    if (!a || !b || !gamma || !beta || !y) return WX_E_INVALID;
+    if (a_stride < D || b_stride < D || (a_stride & 3) || (b_stride & 3)) return WX_E_INVALID;
+    for (const void* p : {(const void*)a, (const void*)b, (const void*)gamma, (const void*)beta, (const void*)y})
+        if (reinterpret_cast<uintptr_t>(p) & 15) return WX_E_INVALID;
+    if (sum_out && (reinterpret_cast<uintptr_t>(sum_out) & 15)) return WX_E_INVALID;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)((rows + 3) / 4));
+    switch (D) {
+        case 256: hipLaunchKernelGGL(add_ln_kernel<1>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
+        case 512: hipLaunchKernelGGL(add_ln_kernel<2>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
+        case 768: hipLaunchKernelGGL(add_ln_kernel<3>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
+        default: hipLaunchKernelGGL(add_ln_kernel<4>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

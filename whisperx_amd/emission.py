@@ -328,6 +328,59 @@ def _fuse_qkv(model: torch.nn.Module) -> None:
             m.forward = types.MethodType(f, m)
 
 
+_ADDLN_WIDTHS = (256, 512, 768, 1024)
+
+
+def _addln_ok(layer, x: torch.Tensor, norms) -> bool:
+    """Whether wx_add_layernorm can stand in for `norm(residual + x)` in this call."""
+    if (os.environ.get("WX_NO_ADDLN") or not x.is_cuda or x.dtype != torch.float32 or torch.is_grad_enabled()
+            or layer.training or x.dim() < 2 or x.shape[-1] not in _ADDLN_WIDTHS or x.stride(-1) != 1):
+        return False
+    D = x.shape[-1]
+    return all(isinstance(n, torch.nn.LayerNorm) and tuple(n.normalized_shape) == (D,) and n.weight is not None
+               and n.bias is not None for n in norms)
+
+
+def _fused_post_ln_layer(self, hidden_states, attention_mask=None, output_attentions=False, **kwargs):
+    """transformers' Wav2Vec2EncoderLayer.forward (post-norm: wav2vec2-base) with both
+    `layer_norm(residual + x)` steps as one wx_add_layernorm each (one pass instead of an add
+    and a LayerNorm kernel)."""
+    if kwargs or not _addln_ok(self, hidden_states, (self.layer_norm, self.final_layer_norm)):
+        return self._wx_orig_forward(hidden_states, attention_mask=attention_mask, output_attentions=output_attentions,
+                                     **kwargs)
+    from . import _lib
+
+    ln, fln = self.layer_norm, self.final_layer_norm
+    h, attn_weights, _ = self.attention(hidden_states, attention_mask=attention_mask, output_attentions=output_attentions)
+    h = self.dropout(h)
+    h = _lib.add_layernorm(hidden_states, h, ln.weight, ln.bias, ln.eps)
+    h = _lib.add_layernorm(h, self.feed_forward(h), fln.weight, fln.bias, fln.eps)
+    return (h, attn_weights) if output_attentions else (h,)
+
+
+def _fused_stable_ln_layer(self, hidden_states, attention_mask=None, output_attentions=False, **kwargs):
+    """transformers' Wav2Vec2EncoderLayerStableLayerNorm.forward (pre-norm: the large models)
+    with `residual + attention` and the feed-forward's `final_layer_norm` of that sum as one
+    wx_add_layernorm that also returns the sum."""
+    if (kwargs or getattr(self, "adapter_layer", None) is not None
+            or not _addln_ok(self, hidden_states, (self.final_layer_norm,))):
+        return self._wx_orig_forward(hidden_states, attention_mask=attention_mask, output_attentions=output_attentions,
+                                     **kwargs)
+    from . import _lib
+
+    fln = self.final_layer_norm
+    h = self.layer_norm(hidden_states)
+    h, attn_weights, _ = self.attention(h, attention_mask=attention_mask, output_attentions=output_attentions)
+    h = self.dropout(h)
+    y, s = _lib.add_layernorm(hidden_states, h, fln.weight, fln.bias, fln.eps, want_sum=True)
+    h = s + self.feed_forward(y)
+    return (h, attn_weights) if output_attentions else (h,)
+
+
+_LAYER_FORWARDS = {"Wav2Vec2EncoderLayer": _fused_post_ln_layer,
+                   "Wav2Vec2EncoderLayerStableLayerNorm": _fused_stable_ln_layer}
+
+
 def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
     """Route the model's Conv1d inference forwards through length-agnostic GEMMs and its
     self-attention through wx_attention_f32 (idempotent).  Returns the same model object."""
@@ -339,6 +392,12 @@ def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
         if isinstance(mod, torch.nn.Conv1d) and not hasattr(mod, "_wx_orig_forward"):
             mod._wx_orig_forward = mod.forward
             mod.forward = types.MethodType(_patched_forward, mod)
+        fwd = _LAYER_FORWARDS.get(type(mod).__name__)
+        if (fwd is not None and not hasattr(mod, "_wx_orig_forward") and hasattr(mod, "attention")
+                and hasattr(mod, "feed_forward") and isinstance(getattr(mod, "layer_norm", None), torch.nn.LayerNorm)
+                and isinstance(getattr(mod, "final_layer_norm", None), torch.nn.LayerNorm)):
+            mod._wx_orig_forward = mod.forward
+            mod.forward = types.MethodType(fwd, mod)
         gn = getattr(mod, "layer_norm", None)
         if (not os.environ.get("WX_NO_CHANNEL_NORM") and isinstance(getattr(mod, "conv", None), torch.nn.Conv1d) and isinstance(gn, torch.nn.GroupNorm)
                 and gn.num_groups == gn.num_channels and gn.num_channels % 4 == 0 and hasattr(mod, "activation")
