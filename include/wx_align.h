@@ -247,6 +247,16 @@ int wx_add_layernorm(const float* a, const float* b, int64_t rows, int32_t D, in
 int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
                      int32_t do_abs, const float* gamma, const float* beta, float eps, float slope,
                      float* y, void* stream);
+/* wx_sincnet_stage with an input affine applied before |.|: x[b][t][c] * in_scale[b] +
+ * in_shift[b][c] (both NULL or both given; in_shift 16-byte aligned), and windows that may
+ * overlap (any x_window_stride >= 0, a multiple of 4).  The producer runs the sinc filterbank
+ * once over the waveform and reads every window's conv output from that shared buffer
+ * (window stride = hop / conv stride rows): the waveform InstanceNorm of the window, a
+ * per-window affine of the input, commutes with the bias-free convolution into
+ * scale * conv(x) + shift_c (shift_c = the norm's offset times filter c's tap sum). */
+int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
+                        int32_t do_abs, const float* in_scale, const float* in_shift, const float* gamma,
+                        const float* beta, float eps, float slope, float* y, void* stream);
 
 /* VAD producer's overlap-add (vad.py:198-240 -> pyannote Inference.aggregate with the
  * multi-label max-over-classes hook): scores [n_chunks, frames_per_chunk, n_classes] fp32

@@ -75,6 +75,7 @@ SIGNATURES = {
     "wx_channel_norm_workspace_bytes": (_sz, [_i32]),
     "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
     "wx_add_layernorm": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
+    "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
@@ -493,9 +494,11 @@ def vad_aggregate(scores: torch.Tensor, start_frames, n_frames: int, missing: fl
     return out[: int(n_frames)]
 
 
-def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slope: float = 0.01) -> torch.Tensor:
-    """wx_sincnet_stage on a time-major conv output x_tm [B, L, C] (row stride C, any window
-    stride): leaky_relu(InstanceNorm1d(MaxPool1d(3, 3)(|x|?))) as [B, L // 3, C] contiguous."""
+def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slope: float = 0.01,
+                  in_scale: Optional[torch.Tensor] = None, in_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """wx_sincnet_stage(_ex) on a time-major conv output x_tm [B, L, C] (row stride C, any
+    window stride, windows may overlap): leaky_relu(InstanceNorm1d(MaxPool1d(3, 3)(|x'|?))) with
+    x' = x * in_scale[b] + in_shift[b, c] when given, as [B, L // 3, C] contiguous."""
     lib = load()
     B, L, C = (int(v) for v in x_tm.shape)
     if x_tm.dtype != torch.float32 or x_tm.stride(2) != 1 or x_tm.stride(1) != C:
@@ -503,9 +506,11 @@ def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slo
     y = torch.empty((B, L // 3, C), dtype=torch.float32, device=x_tm.device)
     g = gamma.detach().contiguous() if gamma is not None else None
     bt = beta.detach().contiguous() if beta is not None else None
+    sc = in_scale.detach().to(torch.float32).contiguous() if in_scale is not None else None
+    sh = in_shift.detach().to(torch.float32).contiguous() if in_shift is not None else None
     with torch.cuda.device(x_tm.device):
-        _check(lib.wx_sincnet_stage(_ptr(x_tm), B, L, C, int(x_tm.stride(0)), int(bool(do_abs)), _ptr(g), _ptr(bt),
-                                    float(eps), float(slope), _ptr(y), _stream(x_tm.device)))
+        _check(lib.wx_sincnet_stage_ex(_ptr(x_tm), B, L, C, int(x_tm.stride(0)), int(bool(do_abs)), _ptr(sc), _ptr(sh),
+                                       _ptr(g), _ptr(bt), float(eps), float(slope), _ptr(y), _stream(x_tm.device)))
     return y
 
 

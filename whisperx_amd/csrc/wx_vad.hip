@@ -35,6 +35,8 @@ struct SincArgs {
     const float* beta;
     float eps, slope;
     float* y;          // [B][Lp][C] contiguous
+    const float* in_scale;  // [B] or null: x * in_scale[b] + in_shift[b][c] before |.|
+    const float* in_shift;  // [B][C] or null
 };
 
 __device__ __forceinline__ float nan_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
@@ -53,6 +55,13 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
         for (int t = r; t < a.Lp; t += R) {
             const float4* src = reinterpret_cast<const float4*>(x + (int64_t)3 * t * a.C) + g;
             float4 u = src[0], v = src[G], w = src[2 * G];
+            if (a.in_scale) {  // the window's input affine (a shared convolution, per-window norm)
+                const float sc = a.in_scale[b];
+                const float4 sh = reinterpret_cast<const float4*>(a.in_shift + (int64_t)b * a.C)[g];
+                u = make_float4(u.x * sc + sh.x, u.y * sc + sh.y, u.z * sc + sh.z, u.w * sc + sh.w);
+                v = make_float4(v.x * sc + sh.x, v.y * sc + sh.y, v.z * sc + sh.z, v.w * sc + sh.w);
+                w = make_float4(w.x * sc + sh.x, w.y * sc + sh.y, w.z * sc + sh.z, w.w * sc + sh.w);
+            }
             if (a.do_abs) {
                 u = make_float4(fabsf(u.x), fabsf(u.y), fabsf(u.z), fabsf(u.w));
                 v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
@@ -113,16 +122,17 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
 
 }  // namespace wxv
 
-extern "C" int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
-                                int32_t do_abs, const float* gamma, const float* beta, float eps, float slope,
-                                float* y, void* stream) {
+extern "C" int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
+                                   int32_t do_abs, const float* in_scale, const float* in_shift, const float* gamma,
+                                   const float* beta, float eps, float slope, float* y, void* stream) {
     using namespace wxv;
-    if (B < 0 || L < 0 || C <= 0 || C > kMaxC || (C & 3) || x_window_stride < L * (int64_t)C) return WX_E_INVALID;
-    if (L / 3 > 0x7fffffff || B > 0x7fffffff) return WX_E_INVALID;
+    // (windows may overlap: x_window_stride < L * C reads a shared time-major output)
+    if (B < 0 || L < 0 || C <= 0 || C > kMaxC || (C & 3) || x_window_stride < 0) return WX_E_INVALID;
+    if (L / 3 > 0x7fffffff || B > 0x7fffffff || (!in_scale != !in_shift)) return WX_E_INVALID;
     const int Lp = (int)(L / 3);
     if (B == 0 || Lp == 0) return WX_OK;  // (an empty output may have no storage)
     if (!x || !y || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y) & 15) ||
-        (x_window_stride & 3))
+        (x_window_stride & 3) || (in_shift && (reinterpret_cast<uintptr_t>(in_shift) & 15)))
         return WX_E_INVALID;
     SincArgs a;
     a.x = x;
@@ -136,7 +146,17 @@ extern "C" int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C,
     a.eps = eps;
     a.slope = slope;
     a.y = y;
+    a.in_scale = in_scale;
+    a.in_shift = in_shift;
     hipLaunchKernelGGL(sinc_stage_kernel, dim3((unsigned)B), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
+                                int32_t do_abs, const float* gamma, const float* beta, float eps, float slope,
+                                float* y, void* stream) {
+    if (x_window_stride < L * (int64_t)C) return WX_E_INVALID;
+    return wx_sincnet_stage_ex(x, B, L, C, x_window_stride, do_abs, nullptr, nullptr, gamma, beta, eps, slope, y,
+                               stream);
 }

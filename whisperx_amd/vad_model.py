@@ -203,8 +203,14 @@ class SincNet(torch.nn.Module):
                                            torch.nn.InstanceNorm1d(60, affine=True)])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.wav_norm1d(x)
+        return self.stages(self.wav_norm1d(x), 0)
+
+    def stages(self, x: torch.Tensor, first: int) -> torch.Tensor:
+        """Stages first..2 on x (the normalised waveform for stage 0, else the previous stage's
+        [B, C, L] output)."""
         for i, (conv, pool, norm) in enumerate(zip(self.conv1d, self.pool1d, self.norm1d)):
+            if i < first:
+                continue
             gemm = _gemm_conv(x)
             if i > 0 and gemm:
                 x = conv1d_batched(x, conv.weight, conv.bias, conv.stride[0])
@@ -219,6 +225,43 @@ class SincNet(torch.nn.Module):
                 x = torch.abs(x)
             x = F.leaky_relu(norm(pool(x)))
         return x
+
+
+def _conv_global(x: torch.Tensor, w: torch.Tensor, stride: int) -> torch.Tensor:
+    """The bias-free strided convolution of one long signal x [n] with filters w [C, k]:
+    [(n - k) // stride + 1, C] time-major, as row-chunked GEMMs on the unfold view (taps
+    zero-padded to a multiple of the stride; ~1 GB of patch rows at a time)."""
+    C, k = w.shape
+    n = x.shape[0]
+    F_out = (n - k) // stride + 1
+    kp = -(-k // stride) * stride
+    xs = F.pad(x, (0, kp - k)) if kp > k else x
+    wp = F.pad(w, (0, kp - k)).t().contiguous()  # [kp, C]
+    pat = xs.unfold(0, kp, stride)[:F_out]  # [F, kp] view
+    out = torch.empty((F_out, C), dtype=x.dtype, device=x.device)
+    rows = max(1, _PATCH_BYTES // (kp * x.element_size()))
+    for r in range(0, F_out, rows):
+        torch.mm(pat[r:r + rows], wp, out=out[r:r + rows])
+    return out
+
+
+def _shared_sinc_ok(model, w: torch.Tensor, hop: int) -> bool:
+    """Whether chunk_scores may run the sinc filterbank once over the waveform
+    (VoiceActivitySegmentation._shared_sinc_scores): this package's PyanNet on a HIP device
+    with the GEMM convolutions and the fused stage epilogue, a window hop that is a multiple
+    of the filterbank stride, and the waveform InstanceNorm using instance statistics
+    (WX_NO_SHARED_SINC=1: one convolution per window)."""
+    if os.environ.get("WX_NO_SHARED_SINC") or not isinstance(model, PyanNet) or not _gemm_conv(w):
+        return False
+    sn = model.sincnet
+    enc, wn = sn.conv1d[0], sn.wav_norm1d
+    if not isinstance(enc, SincEncoder) or hop % enc.stride or os.environ.get("WX_NO_SINC_EPILOGUE"):
+        return False
+    if not isinstance(wn, torch.nn.InstanceNorm1d) or wn.num_features != 1 or (wn.track_running_stats and not wn.training):
+        return False
+    pool, norm = sn.pool1d[0], sn.norm1d[0]
+    probe = torch.empty((1, 80, 3), device=w.device).transpose(1, 2).contiguous().transpose(1, 2)
+    return _fused_epilogue(pool, norm, probe)
 
 
 def _fused_epilogue(pool, norm, x) -> bool:
@@ -266,7 +309,10 @@ class PyanNet(torch.nn.Module):
         return L // 3
 
     def forward(self, waveforms: torch.Tensor) -> torch.Tensor:
-        x = self.sincnet(waveforms)
+        return self.head(self.sincnet(waveforms))
+
+    def head(self, x: torch.Tensor) -> torch.Tensor:
+        """LSTM -> linear layers -> classifier on the SincNet features [B, 60, frames]."""
         x, _ = self.lstm(x.transpose(1, 2))
         for lin in self.linear:
             x = F.leaky_relu(lin(x))
@@ -329,7 +375,9 @@ class VoiceActivitySegmentation:
         n_full, has_last = self.windows(w.shape[1])
         outs = []
         with torch.inference_mode():
-            if n_full:
+            if n_full and _shared_sinc_ok(self.model, w, hop):
+                outs.extend(self._shared_sinc_scores(w, n_full, win, hop))
+            elif n_full:
                 chunks = w.unfold(1, win, hop)[0]  # [n_full, win] (a view)
                 for i in range(0, n_full, self.batch_size):
                     outs.append(self.model(chunks[i:i + self.batch_size].unsqueeze(1).contiguous()))
@@ -338,6 +386,49 @@ class VoiceActivitySegmentation:
                 last = F.pad(last, (0, win - last.shape[1]))
                 outs.append(self.model(last.unsqueeze(1)))
         return torch.cat(outs, 0)
+
+    def _shared_sinc_scores(self, w: torch.Tensor, n_full: int, win: int, hop: int):
+        """The full windows' outputs with the sinc filterbank run once over the waveform.
+
+        Windows overlap tenfold (5 s every 0.5 s), and the filterbank is a bias-free strided
+        convolution, so window b's stage-1 convolution is rows [b * hop / 10, + 7975) of the
+        convolution of the whole span.  The waveform InstanceNorm of the window (pyannote's
+        `wav_norm1d`) is an affine of its input — (x - mean_b) / std_b * g + h — and commutes
+        into the convolution: conv(x_norm)[t, c] = (g / std_b) conv(x)[t, c] + (h - g mean_b /
+        std_b) * sum(filter c).  wx_sincnet_stage_ex applies that per-window affine while it
+        reads the shared output, then |.| -> max-pool -> InstanceNorm -> LeakyReLU as before.
+        Float noise only (the sums are reassociated); stages 2-3 and the rest are unchanged."""
+        sn = self.model.sincnet
+        enc, norm0 = sn.conv1d[0], sn.norm1d[0]
+        wn = sn.wav_norm1d
+        wf = enc.weight()  # [80, 1, k]
+        C, _, k = wf.shape
+        s = enc.stride
+        span = (n_full - 1) * hop + win
+        G = _conv_global(w[0, :span], wf.reshape(C, k), s)  # [F, C] time-major
+        L1 = (win - k) // s + 1
+        fpw = hop // s
+        # the windows' waveform statistics (InstanceNorm1d: biased variance, eps), in fp64
+        chunks = w.unfold(1, win, hop)[0]
+        mean = torch.empty(n_full, dtype=torch.float64, device=w.device)
+        var = torch.empty_like(mean)
+        for i in range(0, n_full, 1024):
+            c = chunks[i:i + 1024].to(torch.float64)
+            var[i:i + 1024], mean[i:i + 1024] = torch.var_mean(c, dim=1, unbiased=False)
+        inv = torch.rsqrt(var + float(wn.eps))
+        g = wn.weight.double()[0] if wn.weight is not None else torch.ones((), dtype=torch.float64, device=w.device)
+        h = wn.bias.double()[0] if wn.bias is not None else torch.zeros((), dtype=torch.float64, device=w.device)
+        scale = (g * inv).float()
+        tapsum = wf.reshape(C, k).double().sum(1)
+        shift = ((h - g * mean * inv)[:, None] * tapsum[None, :]).float()
+        outs = []
+        for i in range(0, n_full, self.batch_size):
+            B = min(self.batch_size, n_full - i)
+            x1 = G.as_strided((B, L1, C), (fpw * C, C, 1), G.storage_offset() + i * fpw * C)
+            y1 = _lib.sincnet_stage(x1, True, norm0.weight, norm0.bias, norm0.eps, in_scale=scale[i:i + B],
+                                    in_shift=shift[i:i + B])
+            outs.append(self.model.head(sn.stages(y1.transpose(1, 2), 1)))
+        return outs
 
     def __call__(self, audio) -> SlidingWindowFeature:
         wav = audio["waveform"] if isinstance(audio, dict) else audio
