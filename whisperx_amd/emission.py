@@ -156,6 +156,17 @@ def _conv1d_gemm(conv: torch.nn.Conv1d, x: torch.Tensor) -> torch.Tensor:
     wg = _tap_weights(conv)  # [G, k, Cg, Cog]
     for bi in range(B):
         xb = xt[bi]  # [Lp, Cin] contiguous
+        if G == 1:  # (the first feature-encoder conv: accumulate into the output, bias first)
+            o3 = out[bi].unsqueeze(0)  # [1, Lout, Cout] view
+            if b is not None:
+                o3.copy_(b.reshape(1, 1, Cout).expand(1, Lout, Cout))
+            else:
+                o3.zero_()
+            for j0 in range(0, k, _TAP_BLOCK):
+                kb = min(_TAP_BLOCK, k - j0)
+                pt = xb[j0:].as_strided((1, Lout, kb * Cg), (Cg, s * Cin, 1))
+                o3.baddbmm_(pt, wg[:, j0:j0 + kb].reshape(1, kb * Cg, Cog))
+            continue
         acc = torch.zeros((G, Lout, Cog), dtype=x.dtype, device=x.device)
         for j0 in range(0, k, _TAP_BLOCK):
             kb = min(_TAP_BLOCK, k - j0)
