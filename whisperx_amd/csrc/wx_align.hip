@@ -74,43 +74,6 @@ __device__ __forceinline__ unsigned shift_in(unsigned w, float c, float s) {
     return r;
 }
 
-// w <- 2w + sign(s - c): the same bit as shift_in wherever s and c are not both infinite
-// with one sign (inf - inf = NaN, whose sign bit is arbitrary) and not (-0, +0): in a
-// segment whose emission rows so far are all finite, every cell a backtrack path reads
-// (DESIGN.md §4.1).  Two VALU instructions with no VCC round trip.
-// Fused with the cell's maximum (one asm block per cell, so that hipcc cannot hoist the
-// eight cells' differences ahead of their uses: +14 VGPRs, a wave per SIMD lost).
-#ifndef WX_OPTFORM
-#define WX_OPTFORM 0
-#endif
-__device__ __forceinline__ void shift_sign_max(unsigned& w, float& cur, float c, float s) {
-#if WX_OPTFORM == 5  // (control: the comparison form itself)
-    w = shift_in(w, c, s);
-    cur = nan_max(s, c);
-#elif WX_OPTFORM == 4  // sign bit in one asm block, the maximum scheduled by hipcc
-    float d;
-    asm("v_sub_f32 %0, %2, %3\n\tv_alignbit_b32 %1, %1, %0, 31" : "=&v"(d), "+v"(w) : "v"(s), "v"(c));
-    cur = nan_max(s, c);
-#elif WX_OPTFORM == 3  // sign bit, scheduled by hipcc
-    w = __builtin_amdgcn_alignbit(w, __builtin_bit_cast(unsigned, s - c), 31);
-    cur = nan_max(s, c);
-#elif WX_OPTFORM == 1  // comparison + add-with-carry, maxNum
-    asm("v_cmp_gt_f32 vcc, %2, %3\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\tv_max_f32 %1, %3, %2"
-        : "+v"(w), "=v"(cur)
-        : "v"(c), "v"(s)
-        : "vcc");
-#elif WX_OPTFORM == 2  // sign bit, maxNum
-    float d;
-    asm("v_sub_f32 %0, %3, %4\n\tv_alignbit_b32 %1, %1, %0, 31\n\tv_max_f32 %2, %3, %4"
-        : "=&v"(d), "+v"(w), "=v"(cur)
-        : "v"(s), "v"(c));
-#else
-    float d;
-    asm("v_sub_f32 %0, %3, %4\n\tv_alignbit_b32 %1, %1, %0, 31\n\tv_maximum3_f32 %2, %3, %4, %4"
-        : "=&v"(d), "+v"(w), "=v"(cur)
-        : "v"(s), "v"(c));
-#endif
-}
 
 // Correctly rounded fp32 exp (the reference's torch-CPU exp is within 1 ULP of it).
 __device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
@@ -517,20 +480,6 @@ struct Forward {
     // LDS read, no wait.  Micro-benchmarks (tools/ubench/step*.hip): a step costs ~20 cycles
     // of one wave alone, each LDS read issued inside the chain ~9 more.
     static constexpr bool kReg = C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS;
-    // Cell pairs through v_pk_add_f32 (the throughput buckets, C even)
-#ifndef WX_PACKED
-    static constexpr bool kPackedAdds = false;
-#else
-    static constexpr bool kPackedAdds = C >= 4 && C % 2 == 0 && MODE == 0;
-#endif
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    // Sign-bit decisions (shift_sign) in the throughput buckets, per chunk while the
-    // segment's emission rows have all been finite (sticky: Forward::rows_finite)
-#ifndef WX_SIGNBITS
-    static constexpr bool kSignBits = false;
-#else
-    static constexpr bool kSignBits = MODE == 0 && !H && !SP && VS != kGatherVS;
-#endif
     static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
     static constexpr int kQS = quad_stride<VS>();
 
@@ -582,9 +531,6 @@ struct Forward {
     }
 
     // All waves of the workgroup call run(); with H, wave W is the helper.
-    // OPT (kSignBits): the decision bits by shift_sign_max while every staged row has been
-    // finite; returns true when one was not (the caller then runs the comparison form).
-    template <bool OPT = false>
     __device__ __forceinline__ static bool run(const SegDesc& d, const float* __restrict__ E, int V,
                                                const int32_t* __restrict__ tok,
                                                unsigned* __restrict__ bits,  // MODE 0: segment's bitmap
@@ -691,7 +637,6 @@ struct Forward {
         // own registers (a loop-carried swap would make hipcc wait for both loads).
         uint64_t xodd[C], xeven[C];
         bool xlost = false;  // SP: a hand-off timed out
-        bool clean = true;   // OPT: every emission row staged so far is finite
 #pragma unroll
         for (int k = 0; k < C; ++k) xodd[k] = xeven[k] = 0;
         // Prefetches are issued by every lane, unconditionally (chunk and lane clamped into the
@@ -816,13 +761,7 @@ struct Forward {
                 st.t += rows;
             } else {
                 (void)OWN;
-                if constexpr (OPT) clean = clean && rows_finite(buf, rows, V);
-                if constexpr (OPT) {
-                    if (vw == 0)
-                        chunk<true, true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
-                    else
-                        chunk<false, true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
-                } else if (vw == 0) {
+                if (vw == 0) {
                     chunk<true>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
                 } else {
                     chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
@@ -879,7 +818,7 @@ struct Forward {
             }
         }
 #endif
-        return xlost || !clean;
+        return xlost;
     }
 
     // ---------------------------------------------------------------- register-resident chunks
@@ -1317,29 +1256,9 @@ struct Forward {
         }
     }
 
-    // Whether rows [0, rows) of a staged chunk buffer (row-major, VS floats a row) are finite in
-    // columns [0, V): lane l scans half a row (16-byte LDS reads), wave-uniform result.
-    __device__ __forceinline__ static bool rows_finite(const float* buf, int rows, int V) {
-        const int l = lane_id();
-        const int r = l >> 1, c0 = (l & 1) * (VS / 2);
-        float m = 0.0f;
-        if (r < rows) {
-#pragma unroll
-            for (int c = 0; c < VS / 2; c += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(buf + r * VS + c0 + c);
-                const int cc = c0 + c;
-                m = __builtin_elementwise_maximum(m, cc < V ? fabsf(v.x) : 0.0f);
-                m = __builtin_elementwise_maximum(m, cc + 1 < V ? fabsf(v.y) : 0.0f);
-                m = __builtin_elementwise_maximum(m, cc + 2 < V ? fabsf(v.z) : 0.0f);
-                m = __builtin_elementwise_maximum(m, cc + 3 < V ? fabsf(v.w) : 0.0f);
-            }
-        }
-        return __all(m < INFINITY);  // (NaN: false)
-    }
-
     // One chunk's steps: unrolled groups of kUnroll with immediate LDS row offsets, then the
     // remainder.  WAVE0: this wave holds column 1 (its left input is column 0).
-    template <bool WAVE0, bool SG = false>
+    template <bool WAVE0>
     __device__ __forceinline__ static void chunk(const char* bb, const float* c0q, int rows, const int (&toff)[C],
                                                  int boff, State& st, int inf_from, bool is_short, bool halo, int f,
                                                  int cnt, bool owner, int N, float* __restrict__ cn,
@@ -1347,13 +1266,13 @@ struct Forward {
         constexpr int kColLds = 3, kColFinite = 1, kColAny = 2;
         if (kPipelined && rows == kChunk) {  // software-pipelined full chunk
             if (!WAVE0)
-                pipelined_chunk<0, SG>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<0>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
             else if (H)
-                pipelined_chunk<kColLds, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColLds>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else if (st.t + kChunk < inf_from)
-                pipelined_chunk<kColFinite, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColFinite>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else
-                pipelined_chunk<kColAny, SG>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
+                pipelined_chunk<kColAny>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             return;
         }
         int r = 0;
@@ -1366,7 +1285,7 @@ struct Forward {
             if (!WAVE0 || H || st.t + kU < inf_from) {  // column 0 from LDS, or finite for the group
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite), SG>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
+                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
                                                                  inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
@@ -1374,7 +1293,7 @@ struct Forward {
             } else {
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    step<kColAny, SG>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
+                    step<kColAny>(gb, ga, u * kRowBytes, boff, c0q, st, inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
                 }
@@ -1391,7 +1310,7 @@ struct Forward {
             const char* ga[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-            step<!WAVE0 ? 0 : (H ? kColLds : kColAny), SG>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
+            step<!WAVE0 ? 0 : (H ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
                                                        cnt, N, tr);
             if (MODE == 0 && owner) cn[st.t] = st.cur[C - 1];
             ++st.t;
@@ -1402,7 +1321,7 @@ struct Forward {
     // computes.  sched_barrier keeps the scheduler from sinking the loads back to their uses
     // (it does, to minimise registers); the waitcnt pass counts them exactly, since LDS
     // returns in order.
-    template <int COL, bool SG = false>
+    template <int COL>
     __device__ __forceinline__ static void pipelined_chunk(const char* bb, const float* c0q, const int (&toff)[C],
                                                            int boff, State& st, int inf_from, bool is_short,
                                                            bool halo, int f, int cnt, bool owner, int N,
@@ -1443,7 +1362,7 @@ struct Forward {
                 c0_of(rw[u + 3], u + 3);
             }
             __builtin_amdgcn_sched_barrier(0);
-            advance<COL, SG>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
+            advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
             hist[u & (kUnroll - 1)] = st.cur[C - 1];
             ++st.t;
             if (MODE == 0 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
@@ -1457,13 +1376,13 @@ struct Forward {
     // One time step t -> t+1 (alignment.py:372-378).  COL: 0 = not the column-1 wave (lane
     // 0's left input is a halo edge, don't-care); column-1 wave: 1 = column 0 finite for the
     // next row, 2 = general column 0, 3 = column 0 read from the helper's LDS row.
-    template <int COL, bool SG = false>
+    template <int COL>
     __device__ __forceinline__ static void step(const char* gb, const char* (&ga)[C], int ro, int boff,
                                                 const float* c0, State& st, int inf_from, bool is_short, bool halo,
                                                 int f, int cnt, int N, float* __restrict__ tr) {
         Row rw;
         load_row<COL>(gb, ga, ro, boff, c0, rw);
-        advance<COL, SG>(gb, ro, c0, rw, st, inf_from, is_short, halo, f, cnt, N, tr);
+        advance<COL>(gb, ro, c0, rw, st, inf_from, is_short, halo, f, cnt, N, tr);
     }
 
     // The LDS operands of one step: em[t, blank], em[t, tok[j-1]] per slot, column 0 (COL 3).
@@ -1482,7 +1401,7 @@ struct Forward {
         if (COL == 1 || COL == 2) rw.c0 = *reinterpret_cast<const float*>(gb + ro);  // em[t, 0]
     }
 
-    template <int COL, bool SG = false>
+    template <int COL>
     __device__ __forceinline__ static void advance(const char* gb, int ro, const float* c0, const Row& rw, State& st,
                                                    int inf_from, bool is_short, bool halo, int f, int cnt, int N,
                                                    float* __restrict__ tr) {
@@ -1505,45 +1424,12 @@ struct Forward {
             left = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, src), 0x138 /* wave_shr:1 */,
                                                                       0xF, 0xF, true));
         }
-        if constexpr (kPackedAdds) {
-            // the stay sums of cell pairs with v_pk_add_f32 (two IEEE fp32 adds per
-            // instruction, the same roundings; the blank operand broadcast).  (The change sums
-            // too — cells (2i+1, 2i+2) from the pair (2i, 2i+1) — cost a v_mov per pair to
-            // gather the two token operands into a register pair.)
-            float s[C], c[C];
 #pragma unroll
-            for (int i = 0; i < C / 2; ++i) {
-                const f32x2 sp = f32x2{st.cur[2 * i], st.cur[2 * i + 1]} + f32x2{eb, eb};
-                s[2 * i] = sp.x;
-                s[2 * i + 1] = sp.y;
-            }
-#pragma unroll
-            for (int k = 0; k < C; ++k) c[k] = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
-#pragma unroll
-            for (int k = C - 1; k >= 0; --k) {
-                if (MODE == 0 && SG) {
-                    float v;
-                    shift_sign_max(st.w[k], v, c[k], s[k]);
-                    st.cur[k] = v;
-                } else {
-                    if (MODE == 0) st.w[k] = shift_in(st.w[k], c[k], s[k]);
-                    st.cur[k] = nan_max(s[k], c[k]);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int k = C - 1; k >= 0; --k) {
-                const float s = st.cur[k] + eb;
-                const float c = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
-                if (MODE == 0 && SG) {
-                    float v;
-                    shift_sign_max(st.w[k], v, c, s);
-                    st.cur[k] = v;
-                } else {
-                    if (MODE == 0) st.w[k] = shift_in(st.w[k], c, s);
-                    st.cur[k] = nan_max(s, c);
-                }
-            }
+        for (int k = C - 1; k >= 0; --k) {
+            const float s = st.cur[k] + eb;
+            const float c = (k == 0 ? left : st.cur[k > 0 ? k - 1 : 0]) + et[k];
+            if (MODE == 0) st.w[k] = shift_in(st.w[k], c, s);
+            st.cur[k] = nan_max(s, c);
         }
         if (COL == 1 || COL == 2) {
             const float e0 = rw.c0;
@@ -2015,10 +1901,7 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
 // Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
 // block, or -1), meaningful in wave 0.
 constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
-#ifndef WX_SPEC_OVERLAP
-#define WX_SPEC_OVERLAP 2
-#endif
-constexpr int kSpecOverlap = WX_SPEC_OVERLAP;  // unrecorded blocks a walker starts above its segment
+constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment (A/B: 3, 4 slower)
 // wave 0's t_start search, in walk blocks (A/B: 1, 3 or 5 within noise)
 constexpr int kSpecArgmaxBlocks = 3;
 template <int CC>
@@ -2354,24 +2237,11 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         sp.xout = xseg + part * kHaloCells;
         sp.xg = xg_lds;
     }
-    if (lane == 0) tsb[2] = 0;
+    if (SP && lane == 0) tsb[2] = 0;
     bool lost = false;
-    using Fwd = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>;
-    if constexpr (Fwd::kSignBits) {
-        // sign-bit decisions first; a segment with a non-finite emission row is run again with
-        // the comparison form (both forms in one chunk loop cost 14 VGPRs: a wave per SIMD)
-        if (!slow) {
-            if (Fwd::template run<true>(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp))
-                tsb[2] = 1;
-            block_fence();
-            if (tsb[2]) {
-                block_fence();  // (every wave has read the flag)
-                Fwd::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp);
-            }
-        }
-    } else if (!slow) {
-        lost = Fwd::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp);
-    }
+    if (!slow)
+        lost = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
+                                                     a.x4 != 0, cm, nullptr, &sp);
     WX_STAMP(1);
     if (SP && lost) tsb[2] = 1;  // (any lane of the consumer or, register-resident kernels, the poller)
     wait_vm();
@@ -2379,16 +2249,12 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     bool failed = false;
     if (SP && !slow) {  // release this part's bits / column-N history; the last part to arrive goes on
         if (lane == 0) {
-#if !defined(WX_DEV_NOFENCE) && !defined(WX_DEV_NOREL)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
             wait_vm();
             const unsigned w = split_arrive(a.arrive + seg, a.epoch, tsb[2] != 0);
             tsb[0] = ((w & 0x7Fu) == (unsigned)P) ? 1 + (int)((w >> 7) & 1u) : 0;
             if (tsb[0]) {
-#if !defined(WX_DEV_NOFENCE) && !defined(WX_DEV_NOACQ)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
                 wait_vm();
                 // every part has arrived: leave the counter clean for the next launch
                 __hip_atomic_store(a.arrive + seg, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2475,11 +2341,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     WX_STAMP_RT(5);
 }
 
-#ifndef WX_MINWAVES
-#define WX_MINWAVES 1
-#endif
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(!H && C == 8 ? WX_MINWAVES : 1, H ? 2 : 8))) void align_dp_kernel(
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
 }
