@@ -1901,7 +1901,7 @@ __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N,
 // Every wave of the workgroup calls it (the barrier); returns wave 0's result (the lowest
 // block, or -1), meaningful in wave 0.
 constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
-constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment (A/B: 3, 4 slower)
+constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment (A/B: 1, 3, 4 slower)
 // wave 0's t_start search, in walk blocks (A/B: 1, 3 or 5 within noise)
 constexpr int kSpecArgmaxBlocks = 3;
 template <int CC>
