@@ -1,0 +1,51 @@
+"""Development tool: time wx_attention_f32 on a 30 s wav2vec2 segment's shape (B=1, H=12/16,
+T=1499, head dim 64), alone and on 8 concurrent streams, for each library given."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+
+
+def run(H, streams, iters=50):
+    import whisperx_amd._lib as L
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    qkv = [torch.randn(1, 1499, H, 64, generator=g).to(dev).transpose(1, 2) for _ in range(3)]
+    ref = torch.nn.functional.scaled_dot_product_attention(*qkv, scale=0.125).transpose(1, 2)
+    out = L.attention_f32(*qkv, 0.125)
+    err = (out - ref).abs().max().item()
+    sts = [torch.cuda.Stream(device=dev) for _ in range(streams)]
+    for _ in range(3):
+        L.attention_f32(*qkv, 0.125)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for i in range(iters):
+        for st in sts:
+            with torch.cuda.stream(st):
+                L.attention_f32(*qkv, 0.125)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / (iters * streams)
+    fl = 4 * H * 1499 * 1499 * 64
+    return dt, fl / dt / 1e12, err
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--child", action="store_true")
+    a = ap.parse_args()
+    if not a.child:  # one subprocess per build: the library path is fixed at import
+        import subprocess
+        for lib in a.libs.split(","):
+            env = dict(os.environ, WX_LIB_PATH=os.path.abspath(lib))
+            subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib], env=env, check=True)
+        sys.exit(0)
+    lib = a.libs
+    for H in (12, 16):
+        for ns in (1, 8):
+            dt, tf, err = run(H, ns)
+            print(f"{os.path.basename(lib):14s} H={H} streams={ns}: {dt*1e6:7.1f} us/call {tf:6.1f} TFLOP/s maxerr {err:.2e}", flush=True)

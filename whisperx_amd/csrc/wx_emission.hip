@@ -123,11 +123,29 @@ struct AttnArgs {
 #endif
 constexpr int kAttnSplit = WX_ATTN_SPLIT;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
 
+#ifndef WX_ATTN_XCD
+#define WX_ATTN_XCD 1
+#endif
+
 __global__ __launch_bounds__(64 * kAttnSplit) void attn_f32_kernel(AttnArgs a) {
     const int T = a.T;
-    const int q0 = blockIdx.x * 32;
-    const int b = blockIdx.y / a.H;
-    const int h = blockIdx.y % a.H;
+    const int nq = (T + 31) / 32;
+    int tile, bh;
+    if (WX_ATTN_XCD) {
+        // 1-D grid, block L runs on XCD L % 8 (round-robin dispatch): hand each XCD a contiguous
+        // run of (head, query tile) units, so the blocks sharing one head's K / V (768 KB at
+        // T = 1499) meet in one XCD's L2 instead of all eight
+        const unsigned L = blockIdx.x, n = gridDim.x, x = L % 8, i = L / 8, q = n / 8, r = n % 8;
+        const unsigned w = x * q + min(x, r) + i;
+        tile = (int)(w % (unsigned)nq);
+        bh = (int)(w / (unsigned)nq);
+    } else {
+        tile = blockIdx.x;
+        bh = blockIdx.y;
+    }
+    const int q0 = tile * 32;
+    const int b = bh / a.H;
+    const int h = bh % a.H;
     const int64_t row0 = (int64_t)b * T;  // o row of query 0 of this batch entry
     const float* Q = a.q + b * a.sqb + h * a.sqh;
     const float* K = a.k + b * a.skb + h * a.skh;
@@ -351,6 +369,7 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     if (B < 0 || H <= 0 || T < 0 || D != 64 || !q || !k || !v || !o || !q_strides || !k_strides || !v_strides)
         return WX_E_INVALID;
     if (B == 0 || T == 0) return WX_OK;
+    if ((int64_t)(T + 31) / 32 * B * H > INT32_MAX) return WX_E_INVALID;  // (one grid dimension)
     const int64_t* st[3] = {q_strides, k_strides, v_strides};
     const float* pt[3] = {q, k, v};
     for (int i = 0; i < 3; ++i) {  // 16-byte rows (float4 reads of Q / K)
@@ -376,8 +395,9 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     a.svh = v_strides[1];
     a.svt = v_strides[2];
     a.scale_log2 = scale * 1.4426950408889634f;
-    hipLaunchKernelGGL(attn_f32_kernel, dim3((unsigned)((T + 31) / 32), (unsigned)(B * H)), dim3(64 * kAttnSplit), 0,
-                       reinterpret_cast<hipStream_t>(stream), a);
+    const dim3 grid = WX_ATTN_XCD ? dim3((unsigned)((int64_t)(T + 31) / 32 * B * H))
+                                  : dim3((unsigned)((T + 31) / 32), (unsigned)(B * H));
+    hipLaunchKernelGGL(attn_f32_kernel, grid, dim3(64 * kAttnSplit), 0, reinterpret_cast<hipStream_t>(stream), a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }
