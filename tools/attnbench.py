@@ -19,7 +19,7 @@ def run(H, streams, iters=50):
     out = L.attention_f32(*qkv, 0.125)
     err = (out - ref).abs().max().item()
     sts = [torch.cuda.Stream(device=dev) for _ in range(streams)]
-    for _ in range(3):
+    for _ in range(30):
         L.attention_f32(*qkv, 0.125)
     torch.cuda.synchronize()
     t = time.perf_counter()
