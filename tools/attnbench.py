@@ -15,6 +15,8 @@ def run(H, streams, iters=50):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     qkv = [torch.randn(1, 1499, H, 64, generator=g).to(dev).transpose(1, 2) for _ in range(3)]
+    if os.environ.get("ATTN_LAYOUT") == "contig":  # [B, H, T, 64] storage: row stride 256 B
+        qkv = [t.contiguous() for t in qkv]
     ref = torch.nn.functional.scaled_dot_product_attention(*qkv, scale=0.125).transpose(1, 2)
     out = L.attention_f32(*qkv, 0.125)
     err = (out - ref).abs().max().item()
@@ -45,7 +47,8 @@ if __name__ == "__main__":
             subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib], env=env, check=True)
         sys.exit(0)
     lib = a.libs
-    for H in (12, 16):
+    run(12, 1, iters=200)  # the first shape timed in a process runs ~2x slow (clocks ramping)
+    for H in (int(x) for x in os.environ.get("ATTN_HS", "12,16").split(",")):
         for ns in (1, 8):
             dt, tf, err = run(H, ns)
             print(f"{os.path.basename(lib):14s} H={H} streams={ns}: {dt*1e6:7.1f} us/call {tf:6.1f} TFLOP/s maxerr {err:.2e}", flush=True)
