@@ -22,6 +22,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("WX_LIB_PATH") or os.path.join(_HERE, "libwxalign.so")
 SRC_PATH = os.path.join(_HERE, "csrc", "wx_align.hip")
 SRC_PATHS = [SRC_PATH, os.path.join(_HERE, "csrc", "wx_emission.hip"), os.path.join(_HERE, "csrc", "wx_vad.hip")]
+INST_PATH = os.path.join(_HERE, "csrc", "wx_align_inst.hip")
+HDR_PATHS = [os.path.join(_HERE, "csrc", "wx_align_dp.h"), INST_PATH]
 INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
 
 MAX_VOCAB = 16384
@@ -92,21 +94,63 @@ class WXError(RuntimeError):
     pass
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/wx_align.hip for gfx950 into libwxalign.so (in-tree)."""
-    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= _newest_source():
-        return LIB_PATH
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", f"-I{INCLUDE_DIR}", "-o", LIB_PATH + ".tmp", *SRC_PATHS]
-    res = subprocess.run(cmd, capture_output=not verbose, text=True)
+N_SHARDS = 8  # instantiation shards of csrc/wx_align_inst.hip (WX_SHARD=0..7)
+BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+
+
+def build(force: bool = False, verbose: bool = False, out: Optional[str] = None, flags=(),
+          jobs: Optional[int] = None) -> str:
+    """Compile the HIP sources for gfx950 into libwxalign.so (in-tree), one translation unit per
+    process: the host ABI, the emission and VAD kernels, and the fused-DP instantiations split
+    over N_SHARDS shards (a single TU takes ~4.5 min; the shards build in parallel).  `flags`
+    adds hipcc flags (A/B variants: tools/build_variant.sh); -DWX_PHASE_TIMING builds the DP in
+    one TU (its debug arrays must be a single copy)."""
+    out = out or LIB_PATH
+    flags = list(flags)
+    if not force and out == LIB_PATH and not flags and os.path.exists(out) and \
+            os.path.getmtime(out) >= _newest_source():
+        return out
+    phase = "-DWX_PHASE_TIMING" in flags
+    tus = [(p, []) for p in SRC_PATHS]
+    if not phase:
+        tus += [(INST_PATH, [f"-DWX_SHARD={k}"]) for k in range(N_SHARDS)]
+    objdir = os.path.join(os.path.dirname(_HERE), "build", "obj", os.path.basename(out).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    jobs = jobs or max(1, min(len(tus), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 4)))
+    cmds, objs = [], []
+    for src, extra in tus:
+        tag = os.path.basename(src).replace(".hip", "") + "".join(e.split("=")[-1] for e in extra)
+        obj = os.path.join(objdir, tag + ".o")
+        objs.append(obj)
+        cmds.append(["hipcc", *BASE_FLAGS, *flags, *extra, f"-I{INCLUDE_DIR}", "-c", src, "-o", obj])
+    pending, running, failed = list(cmds), [], []
+    while pending or running:
+        while pending and len(running) < jobs:
+            c = pending.pop(0)
+            if verbose:
+                print(" ".join(c), flush=True)
+            running.append((c, subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+        c, p = running.pop(0)
+        log = p.communicate()[0]
+        if p.returncode != 0:
+            failed.append((c, log))
+        elif verbose and log.strip():
+            print(log)
+    if failed:
+        for p in [p for _, p in running]:
+            p.wait()
+        c, log = failed[0]
+        raise WXError(f"hipcc failed: {' '.join(c)}\n{log}")
+    link = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", out + ".tmp", *objs]
+    res = subprocess.run(link, capture_output=True, text=True)
     if res.returncode != 0:
-        raise WXError(f"hipcc failed ({res.returncode}):\n{res.stderr}")
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+        raise WXError(f"link failed ({res.returncode}):\n{res.stderr}")
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def _newest_source() -> float:
-    paths = SRC_PATHS + [os.path.join(INCLUDE_DIR, "wx_align.h")]
+    paths = SRC_PATHS + HDR_PATHS + [os.path.join(INCLUDE_DIR, "wx_align.h")]
     return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
 
 
