@@ -8,7 +8,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from whisperx_amd.distributed import (_decode_dictionary, _encode_dictionary, align_corpus,
-                                      broadcast_dictionary, gather_results, pin_rank, rank_cpus, shard_files)
+                                      broadcast_dictionary, gather_results, host_topology, lpt_plan, pin_rank,
+                                      rank_cpus, rank_cpus_numa, shard_files)
 
 
 def test_shard_files_lpt_balanced_and_complete():
@@ -52,6 +53,57 @@ def test_rank_cpus_disjoint_and_covering():
         rank_cpus([0, 1], 2, 2)
 
 
+def test_rank_cpus_numa_split_and_fallback():
+    topo = {"gpu_nodes": [0, 0, 0, 0, 1, 1, 1, 1], "node_cpus": {0: list(range(64)), 1: list(range(64, 128))}}
+    aff = list(range(0, 128, 2))
+    parts = [rank_cpus_numa(aff, r, 8, topo) for r in range(8)]
+    assert sorted(c for p in parts for c in p) == aff  # disjoint, covering
+    for r, p in enumerate(parts):
+        assert p and set(p) <= set(topo["node_cpus"][topo["gpu_nodes"][r]])
+    # the affinity misses node 1 entirely: every rank falls back to plain slices (no overlap)
+    aff2 = list(range(16))
+    assert [rank_cpus_numa(aff2, r, 8, topo) for r in range(8)] == [rank_cpus(aff2, r, 8) for r in range(8)]
+    # unknown topology / fewer GPUs than ranks
+    assert rank_cpus_numa(aff, 3, 8, None) == rank_cpus(aff, 3, 8)
+    assert rank_cpus_numa(aff, 3, 8, {"gpu_nodes": [0, 1], "node_cpus": topo["node_cpus"]}) == rank_cpus(aff, 3, 8)
+
+
+def test_host_topology_from_fake_sysfs(tmp_path, monkeypatch):
+    """KFD nodes (CPU agents skipped), PCI location -> numa_node, node cpulists, visibility."""
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    base = tmp_path / "class/kfd/kfd/topology/nodes"
+    gpus = [(0x0c, 1), (0x8c, 0), (0x1c, 1)]  # (bus, numa) of three GPUs in KFD order
+    (base / "0").mkdir(parents=True)
+    (base / "0" / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for i, (bus, node) in enumerate(gpus, start=1):
+        (base / str(i)).mkdir()
+        (base / str(i) / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        dev = tmp_path / f"bus/pci/devices/0000:{bus:02x}:00.0"
+        dev.mkdir(parents=True)
+        (dev / "numa_node").write_text(f"{node}\n")
+    for node, cl in ((0, "0-3,8-11"), (1, "4-7,12-15")):
+        d = tmp_path / f"devices/system/node/node{node}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cl + "\n")
+    topo = host_topology(str(tmp_path))
+    assert topo["gpu_nodes"] == [1, 0, 1]
+    assert topo["node_cpus"] == {0: [0, 1, 2, 3, 8, 9, 10, 11], 1: [4, 5, 6, 7, 12, 13, 14, 15]}
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,1")
+    assert host_topology(str(tmp_path))["gpu_nodes"] == [1, 0]
+    assert host_topology(str(tmp_path / "missing")) is None
+
+
+def test_lpt_plan_config4():
+    from whisperx_amd import synthetic
+
+    plan = lpt_plan(synthetic.corpus_durations(4))
+    assert set(plan) == {"1", "2", "4", "8"}
+    assert plan["1"]["max_over_mean"] == 1.0
+    for w in ("2", "4", "8"):
+        assert 1.0 <= plan[w]["max_over_mean"] < 1.25
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -60,10 +112,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _fake_numa(world):
+    """The parent's CPUs as two NUMA nodes, GPUs crossed over them (GPU r on node 1 - r % 2)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    half = len(cpus) // 2
+    return {"gpu_nodes": [1 - r % 2 for r in range(world)], "node_cpus": {0: cpus[:half], 1: cpus[half:]}}
+
+
+def _worker(rank, world, port, q, numa=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    pin = pin_rank(rank, world)  # before anything else, as bench.py's ranks do
+    # before anything else, as bench.py's ranks do
+    pin = pin_rank(rank, world, topology=_fake_numa(world) if numa else "auto")
     pin["affinity"] = sorted(os.sched_getaffinity(0))
     pin["torch_threads"] = torch.get_num_threads()
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -77,11 +137,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_broadcast_and_gather():
+@pytest.mark.parametrize("numa", [False, True], ids=["host", "fake_numa"])
+def test_gloo_world2_broadcast_and_gather(numa):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, numa)) for r in range(2)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in procs]
@@ -100,6 +161,11 @@ def test_gloo_world2_broadcast_and_gather():
     for o in outs:
         assert o[3]["affinity"] == o[3]["cpus"]
         assert 1 <= o[3]["torch_threads"] <= len(o[3]["cpus"])
+    if numa and len(parent) >= 2:  # each rank on its GPU's (fake) node: rank 0 -> node 1
+        topo = _fake_numa(2)
+        for r, o in enumerate(outs):
+            assert set(o[3]["cpus"]) <= set(topo["node_cpus"][topo["gpu_nodes"][r]])
+            assert o[3]["numa"] == topo["gpu_nodes"][r]
     merged = outs[0][2]
     assert outs[1][2] is None
     assert sorted(merged) == [0, 1, 2, 3, 4]

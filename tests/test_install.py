@@ -92,11 +92,13 @@ SCRIPT = textwrap.dedent(r'''
     from whisperx_amd import vad_model as amd_vm
     tmp = tempfile.mkdtemp()
     assert lv("cpu", model_fp=os.path.join(tmp, "absent.bin")) == "reference-pyannote-pipeline"
-    pickled = os.path.join(tmp, "lightning.bin")          # pickles a non-tensor object
+    pickled = os.path.join(tmp, "lightning.bin")          # pickles a non-tensor object (Lightning layout)
     torch.save({"state_dict": amd_vm.PyanNet().state_dict(), "loops": SimpleNamespace(epoch=3)}, pickled)
     plain = os.path.join(tmp, "plain.bin")
     torch.save(amd_vm.PyanNet().state_dict(), plain)
-    for fp, want_ref in ((pickled, True), (plain, False)):
+    garbage = os.path.join(tmp, "garbage.bin")            # no tensors to read: the reference's pipeline
+    open(garbage, "wb").write(b"neither zip nor pickle" * 8)
+    for fp, want_ref in ((pickled, False), (plain, False), (garbage, True)):
         digest = hashlib.sha256(open(fp, "rb").read()).hexdigest()   # as if it were the whisperX file
         amd_vm.VAD_SEGMENTATION_URL = "https://x/segmentation/" + digest + "/pytorch_model.bin"
         got = lv("cpu", vad_onset=0.45, model_fp=fp)
@@ -104,7 +106,12 @@ SCRIPT = textwrap.dedent(r'''
             assert got == "reference-pyannote-pipeline", got
         else:
             assert isinstance(got, amd_vm.VoiceActivitySegmentation) and got.hyperparameters["onset"] == 0.45
-    assert ref_vad_calls == [os.path.join(tmp, "absent.bin"), pickled], ref_vad_calls
+    assert ref_vad_calls == [os.path.join(tmp, "absent.bin"), garbage], ref_vad_calls
+    # the default checkpoint (model_fp None) replaced by an exported state_dict of one's own
+    os.environ["WX_VAD_STATE_DICT"] = plain
+    got = lv("cpu", vad_onset=0.4)
+    assert isinstance(got, amd_vm.VoiceActivitySegmentation) and got.hyperparameters["onset"] == 0.4
+    del os.environ["WX_VAD_STATE_DICT"]
     print("rebound", len(rebound))
 ''')
 

@@ -113,3 +113,62 @@ def test_load_vad_model_local_file(tmp_path):
         vad_model.load_vad_model("cpu", model_fp=str(tmp_path / "missing.bin"))
     with pytest.raises(RuntimeError, match="not a regular file"):
         vad_model.load_vad_model("cpu", model_fp=str(tmp_path))
+
+
+# --- a Lightning-style checkpoint whose pickle names code: the no-code reader ----------------
+_SIDE_EFFECTS = []
+
+
+def _record_side_effect(tag):
+    """What unpickling _Trap would call.  The no-code reader must never reach it."""
+    _SIDE_EFFECTS.append(tag)
+    return tag
+
+
+class _Trap:
+    """Pickled into the checkpoint beside the state_dict (as Lightning pickles its hyper-parameter
+    and callback objects): a normal unpickler calls _record_side_effect while loading."""
+
+    def __reduce__(self):
+        return (_record_side_effect, ("executed",))
+
+
+class _Hparams(dict):
+    """A dict subclass with state (NEWOBJ + SETITEMS + BUILD opcodes)."""
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.note = "built"
+
+
+def test_read_checkpoint_tensors_executes_nothing(tmp_path):
+    from whisperx_amd import vad_model
+
+    sd = _synthetic_checkpoint(2)
+    fp = str(tmp_path / "lightning.ckpt")
+    torch.save({"state_dict": sd, "epoch": 7, "trap": _Trap(), "hyper_parameters": _Hparams(lr=1e-3, trap=_Trap()),
+                "callbacks": [_Trap(), {"x": _Trap()}]}, fp)
+    _SIDE_EFFECTS.clear()
+    with pytest.raises(Exception):  # torch's own safe loader refuses the file
+        torch.load(fp, map_location="cpu", weights_only=True)
+    got = vad_model.read_checkpoint_tensors(fp)
+    assert _SIDE_EFFECTS == []  # the trap's callable was never called
+    assert set(got) == set(sd) and all(torch.equal(got[k], sd[k]) for k in sd)
+    # load_vad_model takes that path on its own when weights_only refuses the file
+    pipe = vad_model.load_vad_model("cpu", model_fp=fp, check_sha256=False)
+    assert _SIDE_EFFECTS == []
+    assert torch.equal(pipe.model.classifier.bias, sd["classifier.bias"])
+
+
+def test_unreadable_checkpoint_still_falls_back(tmp_path):
+    from whisperx_amd import vad_model
+
+    fp = tmp_path / "garbage.bin"
+    fp.write_bytes(b"not a checkpoint at all" * 10)
+    with pytest.raises(vad_model.CheckpointNotLoadable):
+        vad_model.load_vad_model("cpu", model_fp=str(fp), check_sha256=False)
+    other = str(tmp_path / "other.ckpt")  # readable, but not a PyanNet state_dict
+    torch.save({"state_dict": {"encoder.weight": torch.zeros(3)}, "trap": _Trap()}, other)
+    with pytest.raises(vad_model.CheckpointNotLoadable):
+        vad_model.load_vad_model("cpu", model_fp=other, check_sha256=False)
+    assert _SIDE_EFFECTS == []

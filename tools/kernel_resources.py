@@ -16,14 +16,19 @@ def notes(so):
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
         txt = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
-    out, cur = [], {}
+    # the metadata keys of a kernel are sorted: those before ".name" (group_segment_fixed_size)
+    # belong to the kernel whose name follows
+    out, cur, pending = [], {}, {}
     for line in txt.splitlines():
         m = re.match(r"\s+\.(name|vgpr_count|sgpr_count|private_segment_fixed_size|group_segment_fixed_size|vgpr_spill_count):\s+(\S+)", line)
         if m:
             k, v = m.groups()
             if k == "name":
-                cur = {"name": v}
+                cur = {"name": v, **pending}
+                pending = {}
                 out.append(cur)
+            elif k < "name":
+                pending[k] = v
             else:
                 cur[k] = v
     names = subprocess.run(["c++filt"], input="\n".join(o["name"] for o in out), capture_output=True,

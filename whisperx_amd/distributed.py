@@ -10,8 +10,9 @@ its own files with no collective on the data path.  The only collectives:
 
 pin_rank splits the host CPUs between the ranks of a node (host CPU per rank —
 Python orchestration and the aggregation — is the scaling limiter): each local rank gets a
-disjoint slice of the process's CPU affinity and an intra-op thread pool of its share of the
-thread budget, so 8 ranks do not each start a pool over every core.
+disjoint slice of the process's CPU affinity, taken from its GPU's NUMA node when the host
+exposes the KFD topology, and an intra-op thread pool of its share of the thread budget, so 8
+ranks do not each start a pool over every core.
 
 shard_files balances mixed-length corpora (BASELINE config 4: 40 files of 1-60 min)
 longest-processing-time first: files sorted by duration (descending, index as tie
@@ -66,23 +67,120 @@ def rank_cpus(cpus: Sequence[int], local_rank: int, local_world: int) -> List[in
     return cpus[local_rank * n // local_world:(local_rank + 1) * n // local_world]
 
 
-def pin_rank(local_rank: Optional[int] = None, local_world: Optional[int] = None) -> dict:
-    """Pin this rank to its disjoint CPU slice and size torch's intra-op pool to its share of
-    the thread budget.  Call before any GPU work (HIP's runtime threads inherit the affinity).
-    Defaults: LOCAL_RANK / LOCAL_WORLD_SIZE from torchrun.  Returns {"cpus", "threads"}."""
+def _parse_cpulist(text: str) -> List[int]:
+    out: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        out.extend(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def _visible(ids: List[int], var: str) -> List[int]:
+    v = os.environ.get(var, "").strip()
+    if not v:
+        return ids
+    try:
+        return [ids[int(x)] for x in v.split(",") if x.strip() != ""]
+    except (ValueError, IndexError):  # UUIDs or out-of-range entries: cannot map, keep all
+        return ids
+
+
+def host_topology(sysfs: str = "/sys") -> Optional[dict]:
+    """{"gpu_nodes": NUMA node of each visible GPU in HIP's order, "node_cpus": {node: [cpus]}}
+    from the KFD topology (GPU agents in node order, as ROCr enumerates them; PCI location ->
+    the device's numa_node) filtered by ROCR_/HIP_/CUDA_VISIBLE_DEVICES, or None when the host
+    does not expose it.  Reads sysfs only: no HIP call, so it can run before pinning."""
+    base = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
+    try:
+        nodes = sorted(int(n) for n in os.listdir(base) if n.isdigit())
+    except OSError:
+        return None
+    gpus: List[int] = []
+    for n in nodes:
+        try:
+            with open(os.path.join(base, str(n), "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue  # a CPU agent
+        loc, dom = int(props.get("location_id", "0")), int(props.get("domain", "0"))
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+        try:
+            with open(os.path.join(sysfs, "bus/pci/devices", bdf, "numa_node")) as f:
+                gpus.append(int(f.read().strip()))
+        except (OSError, ValueError):
+            gpus.append(-1)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        gpus = _visible(gpus, var)
+    if not gpus or any(g < 0 for g in gpus):
+        return None
+    node_cpus = {}
+    for g in set(gpus):
+        try:
+            with open(os.path.join(sysfs, f"devices/system/node/node{g}/cpulist")) as f:
+                node_cpus[g] = _parse_cpulist(f.read())
+        except OSError:
+            return None
+    return {"gpu_nodes": gpus, "node_cpus": node_cpus}
+
+
+def rank_cpus_numa(cpus: Sequence[int], local_rank: int, local_world: int, topo: Optional[dict]) -> List[int]:
+    """Local rank's CPUs from its GPU's NUMA node: the node's CPUs within `cpus`, split between
+    the ranks whose GPUs share that node (rank_cpus).  Disjoint across ranks.  Falls back to
+    rank_cpus over all of `cpus` for every rank when the topology is unknown, covers fewer GPUs
+    than ranks, or any rank's node has none of `cpus` (a mixed rule could overlap)."""
+    if local_world < 1 or not 0 <= local_rank < local_world:
+        raise ValueError(f"local rank {local_rank} outside a node of {local_world}")
+    allowed = set(int(c) for c in cpus)
+    if topo and len(topo.get("gpu_nodes", [])) >= local_world:
+        nodes = [topo["gpu_nodes"][r] for r in range(local_world)]
+        share = {n: sorted(allowed & set(topo["node_cpus"].get(n, []))) for n in set(nodes)}
+        if all(share[n] for n in nodes):
+            peers = [r for r in range(local_world) if nodes[r] == nodes[local_rank]]
+            return rank_cpus(share[nodes[local_rank]], peers.index(local_rank), len(peers))
+    return rank_cpus(cpus, local_rank, local_world)
+
+
+def pin_rank(local_rank: Optional[int] = None, local_world: Optional[int] = None,
+             topology: Optional[dict] = "auto") -> dict:
+    """Pin this rank to its disjoint CPU slice — on its GPU's NUMA node when the host exposes
+    the topology (host_topology; `topology` overrides it, None disables it) — and size torch's
+    intra-op pool to its share of the thread budget.  Call before any GPU work (HIP's runtime
+    threads inherit the affinity).  Defaults: LOCAL_RANK / LOCAL_WORLD_SIZE from torchrun.
+    Returns {"cpus", "threads", "numa"}."""
     lr = int(os.environ.get("LOCAL_RANK", "0")) if local_rank is None else int(local_rank)
     lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if local_world is None else int(local_world)
     budget = thread_budget()
     if not hasattr(os, "sched_getaffinity"):
         threads = max(1, budget // max(lw, 1))
         torch.set_num_threads(threads)
-        return {"cpus": None, "threads": threads}
-    mine = rank_cpus(os.sched_getaffinity(0), lr, lw)
+        return {"cpus": None, "threads": threads, "numa": None}
+    topo = host_topology() if topology == "auto" else topology
+    aff = os.sched_getaffinity(0)
+    mine = rank_cpus_numa(aff, lr, lw, topo)
+    numa = None
+    if topo and len(topo["gpu_nodes"]) > lr and set(mine) <= set(topo["node_cpus"].get(topo["gpu_nodes"][lr], [])):
+        numa = topo["gpu_nodes"][lr]
     if mine:
         os.sched_setaffinity(0, mine)
     threads = max(1, min(len(mine) or 1, budget // max(lw, 1)))
     torch.set_num_threads(threads)
-    return {"cpus": mine, "threads": threads}
+    return {"cpus": mine, "threads": threads, "numa": numa}
+
+
+def lpt_plan(durations: Sequence[float], worlds=(1, 2, 4, 8)) -> dict:
+    """Predicted load balance of shard_files: max / mean rank load per world size (the
+    strong-scaling ceiling of a per-file corpus run is world / (max/mean))."""
+    out = {}
+    for w in worlds:
+        loads = [sum(float(durations[i]) for i in s) for s in shard_files(durations, w)]
+        mean = sum(loads) / w
+        out[str(w)] = {"max_over_mean": max(loads) / mean if mean > 0 else 1.0,
+                       "max_load_s": max(loads), "ideal_speedup": w / (max(loads) / mean) if mean > 0 else float(w)}
+    return out
 
 
 def _encode_dictionary(d: Dict[str, int]) -> torch.Tensor:

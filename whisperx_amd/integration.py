@@ -18,6 +18,7 @@ or a user's own pipeline runs:
 from __future__ import annotations
 
 import importlib
+import os
 import sys
 from typing import Dict, List, Optional, Tuple
 
@@ -27,11 +28,18 @@ def _vad_loader(reference_loader):
     called at asr.py:347): this package's producer (PyanNet + wx_vad_aggregate, scores kept on
     the device) when the checkpoint loads without executing anything from it; otherwise —
     a pickled Lightning checkpoint, another key layout, or no local file (the reference then
-    downloads it) — the reference's own pyannote pipeline, with a one-line notice."""
+    downloads it) — the reference's own pyannote pipeline, with a one-line notice.  The default
+    checkpoint (model_fp None: the whisperX file the reference caches) is read tensors-only by
+    vad_model.read_checkpoint_tensors; WX_VAD_STATE_DICT names a state_dict file of one's own to
+    use instead (no SHA256 check).  A digest mismatch raises RuntimeError, as the reference does."""
     from . import vad_model
 
     def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=None, model_fp=None):
+        own = os.environ.get("WX_VAD_STATE_DICT")  # an exported state_dict of one's own (no digest check)
         try:
+            if own and model_fp is None:
+                return vad_model.load_vad_model(device, vad_onset=vad_onset, vad_offset=vad_offset,
+                                                use_auth_token=use_auth_token, model_fp=own, check_sha256=False)
             return vad_model.load_vad_model(device, vad_onset=vad_onset, vad_offset=vad_offset,
                                             use_auth_token=use_auth_token, model_fp=model_fp)
         except (vad_model.CheckpointNotLoadable, FileNotFoundError) as e:

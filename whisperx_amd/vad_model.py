@@ -34,6 +34,8 @@ from __future__ import annotations
 import hashlib
 import math
 import os
+import pickle
+import types
 from typing import Optional
 
 import numpy as np
@@ -455,6 +457,84 @@ class CheckpointNotLoadable(RuntimeError):
     load_vad_model then falls back to the reference's own pyannote pipeline."""
 
 
+class _Inert:
+    """Stands for every global a checkpoint names outside torch's tensor-rebuild allow-list
+    (Lightning / pyannote classes, hyper-parameter objects, anything else): constructing it,
+    calling it, setting its state or adding items to it records nothing and runs nothing."""
+
+    def __init__(self, *args, **kwargs):
+        pass
+
+    def __call__(self, *args, **kwargs):
+        return type(self)()
+
+    def __setstate__(self, state):
+        pass
+
+    def __setitem__(self, key, value):
+        pass
+
+    def append(self, x):
+        pass
+
+    def extend(self, xs):
+        pass
+
+
+def _allowed_globals() -> dict:
+    """torch's own weights_only allow-list (tensor/parameter/storage rebuilds, dtypes, Size,
+    OrderedDict): the globals a tensor checkpoint needs and nothing that runs code."""
+    try:
+        from torch._weights_only_unpickler import _get_allowed_globals
+
+        return dict(_get_allowed_globals())
+    except Exception:  # (a torch without it: the tensor rebuilds by name)
+        import collections
+        import torch._utils as tu
+
+        out = {f"torch._utils.{n}": getattr(tu, n) for n in ("_rebuild_tensor", "_rebuild_tensor_v2",
+                                                              "_rebuild_parameter") if hasattr(tu, n)}
+        out["collections.OrderedDict"] = collections.OrderedDict
+        out["torch.Size"] = torch.Size
+        return out
+
+
+class _NoCodeUnpickler(pickle.Unpickler):
+    """find_class returns torch's tensor-rebuild globals by name and an inert stand-in
+    (_Inert subclass) for every other global, so loading executes nothing from the file."""
+
+    _ALLOWED = None
+
+    def find_class(self, module, name):
+        if _NoCodeUnpickler._ALLOWED is None:
+            _NoCodeUnpickler._ALLOWED = _allowed_globals()
+        obj = _NoCodeUnpickler._ALLOWED.get(f"{module}.{name}")
+        if obj is not None:
+            return obj
+        return type(f"Inert[{module}.{name}]"[:200], (_Inert,), {})
+
+
+def _nocode_load(f, **kwargs):
+    return _NoCodeUnpickler(f, **kwargs).load()
+
+
+_NOCODE_PICKLE = types.SimpleNamespace(__name__="whisperx_amd.nocode_pickle", Unpickler=_NoCodeUnpickler,
+                                       load=_nocode_load)
+
+
+def read_checkpoint_tensors(path: str) -> dict:
+    """The tensors of a pickled checkpoint (e.g. pyannote's Lightning file) without executing
+    anything from it: torch.load's zip/storage handling with an unpickler that allow-lists
+    torch's tensor-rebuild globals and maps every other global to an inert stub.  Returns the
+    'state_dict' entry when there is one (Lightning layout), else the loaded mapping; only
+    tensor values are kept."""
+    obj = torch.load(path, map_location="cpu", pickle_module=_NOCODE_PICKLE, weights_only=False)
+    sd = obj.get("state_dict", obj) if isinstance(obj, dict) else None
+    if not isinstance(sd, dict):
+        raise CheckpointNotLoadable(f"{path}: no state_dict mapping in the checkpoint")
+    return {k: v for k, v in sd.items() if isinstance(k, str) and torch.is_tensor(v)}
+
+
 VAD_SEGMENTATION_URL = ("https://whisperx.s3.eu-west-2.amazonaws.com/model_weights/segmentation/"
                         "0b5b3216d60a2d32fc086b47ea8c67589aaeb26b7e07fcbe620d6d0b83e209ea/pytorch_model.bin")
 
@@ -465,10 +545,12 @@ def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=Non
     torch hub's whisperx-vad-segmentation.bin, where the reference caches its download) is
     checked against the SHA256 in VAD_SEGMENTATION_URL like the reference does
     (`check_sha256=False` for a checkpoint of one's own), read with
-    ``torch.load(..., weights_only=True)`` (nothing in the file is executed) and loaded into a
-    PyanNet; returns the producer pipeline with the reference's hyper-parameters.  A file that
-    is absent raises FileNotFoundError (offline: there is nothing to fetch it from); one that
-    torch.load(weights_only=True) refuses, or whose keys are not PyanNet's, raises
+    ``torch.load(..., weights_only=True)`` or — a pickled Lightning checkpoint, which that
+    refuses — read_checkpoint_tensors (torch's tensor-rebuild globals, inert stubs for every
+    other global: nothing in the file is executed either way) and loaded into a PyanNet;
+    returns the producer pipeline with the reference's hyper-parameters.  A file that is
+    absent raises FileNotFoundError (offline: there is nothing to fetch it from); one whose
+    tensors cannot be read that way, or whose keys are not PyanNet's, raises
     CheckpointNotLoadable.  Loading the real whisperX checkpoint (a pyannote/Lightning file)
     is untested here — pyannote and the file are absent — so its parity is unpinned: the
     expected layout is pyannote 3.1's PyanNet state_dict (sincnet.wav_norm1d,
@@ -490,10 +572,12 @@ def load_vad_model(device, vad_onset=0.500, vad_offset=0.363, use_auth_token=Non
     try:
         ckpt = torch.load(model_fp, map_location="cpu", weights_only=True)
     except Exception as e:  # a Lightning checkpoint with pickled non-tensor objects
-        raise CheckpointNotLoadable(
-            f"{model_fp}: torch.load(weights_only=True) refused the file ({str(e).splitlines()[0][:200]}); "
-            f"this loader executes nothing from a checkpoint: export its 'state_dict' entry (tensors "
-            f"only, pyannote's key names) with tooling you trust and pass that file") from e
+        try:  # its tensors through the no-code unpickler (stubs for every other global)
+            ckpt = read_checkpoint_tensors(model_fp)
+        except Exception as e2:
+            raise CheckpointNotLoadable(
+                f"{model_fp}: torch.load(weights_only=True) refused the file ({str(e).splitlines()[0][:160]}) and "
+                f"its tensors could not be read without executing it ({str(e2).splitlines()[0][:160]})") from e2
     try:
         model = PyanNet.from_pyannote_state_dict(ckpt)
     except (KeyError, RuntimeError, AttributeError) as e:
