@@ -599,6 +599,47 @@ def _allreduce(vals, op):
 _allreduce.dev = torch.device("cpu")
 
 
+def host_share_leg(k):
+    """Child process of the N=1 bench (bench.py --host-share-leg K): rank 0 of a K-GPU node as the
+    config-4 corpus run would make it — pinned with distributed.pin_rank(0, K) before any GPU
+    call (its NUMA node's share of the host CPUs, 1/K of the threads), then its LPT shard of the
+    10 h corpus — so that one GPU measures the host share a rank has at K GPUs.  Prints one
+    JSON line."""
+    from whisperx_amd import synthetic
+    from whisperx_amd.distributed import pin_rank, shard_files
+
+    pin = pin_rank(0, k)
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    res = corpus_config4(device, 0, k, False)
+    durs = synthetic.corpus_durations(4)
+    loads = [sum(durs[i] for i in s) for s in shard_files(durs, k)]
+    shard_audio = loads[0]
+    # strong-scaling prediction for K GPUs: every rank at rank 0's rate, the slowest LPT share
+    rate = shard_audio / res["wall_s"]
+    pred_wall = max(loads) / rate
+    print(json.dumps({"ranks_modelled": k, "rank": 0, "cpus": len(pin["cpus"] or []), "threads": pin["threads"],
+                      "numa_node": pin["numa"], "shard_audio_sec": shard_audio, "files": res["files"],
+                      "segments": res["segments"], "wall_s": res["wall_s"], "audio_sec_per_s": rate,
+                      "predicted_node_audio_sec_per_s": float(sum(durs)) / pred_wall,
+                      "predicted_node_wall_s": pred_wall,
+                      "note": f"rank 0 of a {k}-GPU node on one GPU: pin_rank(0, {k}) host share, its LPT shard of "
+                              f"the config-4 corpus; prediction = total audio / (largest shard / this rate)"}),
+          flush=True)
+    return 0
+
+
+def _host_share(k, timeout=300):
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--host-share-leg", str(k)],
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(lines[-1])
+
+
 def _spawn_ranks(args):
     """--gpus N > 1 without a torchrun environment: launch N ranks as a child torchrun and
     exit with its status.  The parent never touches the GPU (no HIP init before the child)."""
@@ -626,7 +667,10 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-scale", action="store_true")
     ap.add_argument("--no-corpus", action="store_true", help="skip the config-4 10 h corpus leg")
+    ap.add_argument("--host-share-leg", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.host_share_leg:
+        return host_share_leg(args.host_share_leg)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_spawn_ranks(args))
@@ -733,6 +777,17 @@ def main():
         extra = {}
         if corpus is not None:
             extra["config4_10h_corpus"] = corpus
+        if not args.no_corpus:
+            from whisperx_amd import synthetic
+            from whisperx_amd.distributed import lpt_plan
+
+            extra["lpt_plan"] = lpt_plan(synthetic.corpus_durations(4))
+            if world == 1:
+                log("bench: config-4 host-share leg (rank 0 of 8) ...")
+                try:
+                    extra["config4_host_share"] = _host_share(8)
+                except Exception as e:  # never let the secondary leg hide the primary line
+                    extra["config4_host_share"] = {"error": repr(e)[:300]}
         if not args.no_scale and world == 1:
             # saturated batch: enough segments in flight to fill the chip (roofline regime)
             rng2 = np.random.default_rng(77)

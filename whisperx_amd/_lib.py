@@ -582,7 +582,10 @@ def add_layernorm(a: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: t
     D = int(a.shape[-1])
     if tuple(a.shape) != tuple(b.shape):
         raise WXError(f"add_layernorm: shapes differ ({tuple(a.shape)}, {tuple(b.shape)})")
-    a2, b2 = a.reshape(-1, D), b.reshape(-1, D)
+    # the kernel reads 16-byte vectors: 16-byte aligned rows (row stride a multiple of 4 floats);
+    # an unaligned view is copied (contiguous) rather than refused
+    a2, b2 = (t if t.data_ptr() % 16 == 0 and (t.shape[0] <= 1 or t.stride(0) % 4 == 0) and t.stride(1) == 1
+              else t.contiguous() for t in (a.reshape(-1, D), b.reshape(-1, D)))
     rows = int(a2.shape[0])
     y = torch.empty(a.shape, dtype=torch.float32, device=a.device)
     s = torch.empty_like(y) if want_sum else None

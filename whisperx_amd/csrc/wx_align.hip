@@ -1300,10 +1300,12 @@ size_t xg_bytes(int32_t S, int64_t sum_T) {
     return align_up((size_t)(sum_T / kChunk + S + 2) * (kMaxParts - 1) * kHaloCells * 8u, 256);
 }
 size_t arrive_bytes(int32_t S) { return align_up((size_t)(S + 1) * 8u, 256); }
+// checkpointed kernels' column-0 cumsum per chunk: (floor(row0/32) + seg + q) doubles
+size_t c0acc_bytes(int32_t S, int64_t sum_T) { return align_up((size_t)(sum_T / kChunk + S + 2) * 8u, 256); }
 
 size_t wx_align_dp_workspace_bytes(int32_t S, int64_t sum_T, int64_t max_N) {
     return bitmap_bytes(S, sum_T, max_N, nullptr) + align_up((size_t)(sum_T + 1) * 4u, 256) + cmask_bytes(S, sum_T) +
-           cn_bytes(S, sum_T) + xg_bytes(S, sum_T) + arrive_bytes(S);
+           cn_bytes(S, sum_T) + c0acc_bytes(S, sum_T) + xg_bytes(S, sum_T) + arrive_bytes(S);
 }
 
 // CUs of the current device (cached per device).
@@ -1406,7 +1408,8 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
     a.cmask = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(workspace) + bm +
                                           align_up((size_t)(sum_T + 1) * 4u, 256));
     a.cn = reinterpret_cast<float*>(reinterpret_cast<char*>(a.cmask) + cmask_bytes(S, sum_T));
-    a.xg = reinterpret_cast<uint64_t*>(handoff ? handoff : reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
+    a.c0acc = reinterpret_cast<double*>(reinterpret_cast<char*>(a.cn) + cn_bytes(S, sum_T));
+    a.xg = reinterpret_cast<uint64_t*>(handoff ? handoff : reinterpret_cast<char*>(a.c0acc) + c0acc_bytes(S, sum_T));
     a.arrive = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.xg) + xg_bytes(S, sum_T));
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     a.mode = align_mode(S, mode);

@@ -375,6 +375,10 @@ __device__ unsigned long long wx_cq[8192 * 48 * 3];
 // The trellis forward pass shared by the fused and the materialising kernels.
 //   MODE 0: fused — per-cell 32-step decision words -> bits, column N history -> cn.
 //   MODE 1: materialise — write every trellis row (get_trellis).
+//   MODE 2: checkpointed — no decision bits: at each chunk start (row 32q) every owner lane
+//           stores its C cell values in the bitmap's word layout, and wave 0 the fp64
+//           column-0 cumsum; the walk recomputes each block's band from them (CkSrc).  A
+//           cell step is then 3 VALU (add, DPP add, maximum) instead of 5.
 //
 // W > 1 waves split the columns of one segment with a chunk halo instead of a per-step
 // exchange: wave w >= 1 spends its first HL = ceil(32/C) lanes re-computing the last HL
@@ -471,7 +475,11 @@ struct Forward {
     // Software-pipelined LDS operands where the extra registers keep the occupancy that
     // matters: latency buckets (2 waves per SIMD by design) and one-wave buckets up to
     // C = 8; the multi-wave C = 8 buckets lose a wave per SIMD to them (A/B: -17%).
-    static constexpr bool kPipelined = H || (MODE == 0 && (C <= 6 || (C == 8 && W == 1)));
+    static constexpr bool kPipelined = H || (MODE != 1 && (C <= 6 || (C == 8 && W == 1)));
+    // Column 0 (tr[t][0]) read from LDS by the column-1 wave (COL kColLds): the helper wave
+    // computes it (H), or — checkpointed multi-wave kernels — DP wave 1 does, a chunk ahead
+    // (c0_make): the fp64 cumsum per step otherwise paced wave 0 (+25% steps in the phase timing).
+    static constexpr bool kC0Lds = H || (MODE == 2 && W >= 2);
     using Geo = Geometry<C, (SP ? 2 : W)>;  // SP: always a halo (the waves span P parts)
     // Steps per unrolled group of the non-pipelined chunk (hipcc hoists the group's LDS
     // loads; a multiple of 4: column-N history is stored as float4).
@@ -545,12 +553,35 @@ struct Forward {
                                                float* xh /* 2 * W * 64: chunk halo copies */, bool x4,
                                                const ColMap& cm /* VS == kGatherVS: column map */,
                                                float* rst = nullptr /* MODE 1: W * 64 * C row staging */,
-                                               const Split* sp = nullptr /* SP */) {
+                                               const Split* sp = nullptr /* SP */,
+                                               double* c0acc = nullptr /* MODE 2: column-0 cumsum per chunk */) {
         const int wv = uniform((int)threadIdx.x >> 6);
         const int vw = SP ? sp->p * W + wv : wv;  // virtual wave (SP: across parts)
         const int lanes = SP ? sp->lanes : kLanes;
         const int T = d.T, N = d.N;
         const int nch = (T + kChunk - 1) / kChunk;
+        // checkpointed multi-wave kernels: wave 1 makes column 0 of chunk q + 1 (into c0b, and
+        // its cumsum at row 32 (q + 1) into c0acc) after its chunk-q steps, from em[., 0] loaded a
+        // chunk ahead: the kReg helper's lane-parallel, order-preserving fp64 prefix (col0_pre)
+        const bool c0prod = MODE == 2 && W >= 2 && wv == 1;
+        double c0a = 0.0;  // S(32 q) of the next chunk to make (uniform)
+        float c0e = 0.0f;
+        const int l0 = lane_id();
+        auto c0_load = [&](int qq) { return E[(int64_t)min(qq * kChunk + (l0 & 31), T - 1) * V]; };
+        auto c0_make = [&](int qq, float e) {
+            float x = l0 >= 32 ? e : 0.0f;
+            double a = c0a;
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) {
+                a += (double)x;
+                x = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x130 /* wave_shl:1 */,
+                                                                       0xF, 0xF, true));
+            }
+            if (l0 == 0) c0acc[qq] = c0a;
+            if (l0 < kChunk) c0b[(qq & 1) * kChunk + l0] = col0_value(qq * kChunk + l0, a, T, N);
+            c0a = __shfl(a, kChunk);
+        };
+        if (c0prod && nch > 0) c0_make(0, c0_load(0));  // (before barrier 0)
         if (H && wv >= W) {
             // NH == 2 (split kernels): wave W stages, wave W + 1 runs column 0's fp64 chain;
             // one helper doing both paced part 0 (it reached every chunk barrier last)
@@ -578,6 +609,7 @@ struct Forward {
             for (int q = 0; q < nch; ++q) {
                 wait_vm();
                 __syncthreads();
+                if (c0prod && q + 1 < nch) c0_make(q + 1, c0_load(q + 1));
                 if (!H && q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
                                       lds + ((q + 1) % kBufs) * kBufFloats, x4, cm);
@@ -740,14 +772,27 @@ struct Forward {
                     xpre[k] = granule_load(sp->xin + (int64_t)min(q + 2, nch - 1) * sp->xstride + xl + k);
             }
             if (SP && MODE == 0 && q > 0 && !halo && g < L.G) store_deferred(q - 1);
+            if constexpr (MODE == 2) {
+                // checkpoint row 32q (before the chunk's steps; after the barrier, so that the
+                // next chunk's vmcnt wait finds these stores a chunk old): the owner lanes' cells
+                // in the bitmap word layout, and the fp64 cumsum behind column 0 (wave 0: every
+                // lane holds it, alignment.py:368)
+                if (!halo && g < L.G) {
+                    float* ck = reinterpret_cast<float*>(bits);
+#pragma unroll
+                    for (int k = 0; k < C; ++k) ck[((int64_t)q * C + k) * lanes + g] = st.cur[k];
+                }
+                if (!kC0Lds && vw == 0 && l == 0) c0acc[q] = st.acc;
+            }
+            if (c0prod && q + 1 < nch) c0e = c0_load(q + 1);  // (consumed after this chunk's steps)
             if (!H) {
                 if (q + 1 < nch)
                     stage_rows<VS, W>(E, V, (q + 1) * kChunk, min(kChunk, T - (q + 1) * kChunk),
                                       lds + ((q + 1) % kBufs) * kBufFloats, x4, cm);
-                if (MODE == 0 && wv == 0 && l < rows) q0[q * kChunk + l] = exp_cr(buf[l * VS]);  // never idle
+                if (MODE != 1 && wv == 0 && l < rows) q0[q * kChunk + l] = exp_cr(buf[l * VS]);  // never idle
             }
             const char* bb = reinterpret_cast<const char*>(buf);
-            const float* c0q = H ? c0b + (q & 1) * kChunk : nullptr;
+            const float* c0q = kC0Lds ? c0b + (q & 1) * kChunk : nullptr;
             WX_T(c3);
             if constexpr (kReg) {
                 if (q == 0) reg_load(o, bb, etq, ebq);
@@ -770,6 +815,7 @@ struct Forward {
                     chunk<false>(bb, c0q, rows, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
                 }
             }
+            if (c0prod && q + 1 < nch) c0_make(q + 1, c0e);  // (read after barrier q + 1)
             WX_T(c4);
 #ifdef WX_PHASE_TIMING
             acc_steps += c4 - c3;
@@ -808,7 +854,7 @@ struct Forward {
             for (int q = 0; q < nch; ++q) chunk_iter(q, xeven, opsA, opsB, BoolTag<true>{});
         }
 #ifdef WX_PHASE_TIMING
-        if (l == 0 && blockIdx.x < 8192 && MODE == 0) {
+        if (l == 0 && blockIdx.x < 8192 && MODE != 1) {
             unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + wv) * 3;
             o[0] = acc_steps;
             o[1] = acc_bar;
@@ -1270,7 +1316,7 @@ struct Forward {
         if (kPipelined && rows == kChunk) {  // software-pipelined full chunk
             if (!WAVE0)
                 pipelined_chunk<0>(bb, c0q, toff, boff, st, inf_from, false, halo, f, cnt, owner, N, cn, tr);
-            else if (H)
+            else if (kC0Lds)
                 pipelined_chunk<kColLds>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
             else if (st.t + kChunk < inf_from)
                 pipelined_chunk<kColFinite>(bb, c0q, toff, boff, st, inf_from, is_short, halo, f, cnt, owner, N, cn, tr);
@@ -1285,10 +1331,10 @@ struct Forward {
 #pragma unroll
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
             float hist[kU];  // column N after each step (owner lane)
-            if (!WAVE0 || H || st.t + kU < inf_from) {  // column 0 from LDS, or finite for the group
+            if (!WAVE0 || kC0Lds || st.t + kU < inf_from) {  // column 0 from LDS, or finite for the group
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
-                    step<!WAVE0 ? 0 : (H ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
+                    step<!WAVE0 ? 0 : (kC0Lds ? kColLds : kColFinite)>(gb, ga, u * kRowBytes, boff, c0q + r + u, st,
                                                                  inf_from, is_short, halo, f, cnt, N, tr);
                     hist[u] = st.cur[C - 1];
                     ++st.t;
@@ -1301,7 +1347,7 @@ struct Forward {
                     ++st.t;
                 }
             }
-            if (MODE == 0 && owner) {  // rows t-kU+1 .. t at cn[t-kU .. t-1] (16-byte aligned)
+            if (MODE != 1 && owner) {  // rows t-kU+1 .. t at cn[t-kU .. t-1] (16-byte aligned)
                 float4* o = reinterpret_cast<float4*>(cn + st.t - kU);
 #pragma unroll
                 for (int i = 0; i < kU / 4; ++i)
@@ -1313,9 +1359,9 @@ struct Forward {
             const char* ga[C];
 #pragma unroll
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
-            step<!WAVE0 ? 0 : (H ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
+            step<!WAVE0 ? 0 : (kC0Lds ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
                                                        cnt, N, tr);
-            if (MODE == 0 && owner) cn[st.t] = st.cur[C - 1];
+            if (MODE != 1 && owner) cn[st.t] = st.cur[C - 1];
             ++st.t;
         }
     }
@@ -1368,7 +1414,7 @@ struct Forward {
             advance<COL>(bb, u * kRowBytes, c0q + u, rw[u], st, inf_from, is_short, halo, f, cnt, N, tr);
             hist[u & (kUnroll - 1)] = st.cur[C - 1];
             ++st.t;
-            if (MODE == 0 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
+            if (MODE != 1 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
                 float4* o = reinterpret_cast<float4*>(cn + st.t - kUnroll);
                 o[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
                 o[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
@@ -1714,6 +1760,222 @@ __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
 // where segment k's walker stood after the same block — or enters segment k on its guessed
 // column — the rest of that segment's change masks, end column and result are the true
 // walk's, and wave 0 jumps to the segment's end.
+// Decision words from the forward's bitmap (load_window): block bb's window issued at column
+// A holds columns A - lane (lo) and A - 64 - lane (hi); at use the 64 lanes from the walk's
+// offset are gathered (two ds_bpermutes, skipped while the block fits the first word).
+template <int CC>
+struct BitSrc {
+    const unsigned* bits;
+    Layout lay;
+    struct Win {
+        unsigned lo, hi;
+        int A;
+    };
+    __device__ __forceinline__ void issue(Win& w, int bb, int A) const {
+        w.A = uniform(A);
+        w.lo = load_window<CC>(bits, lay, bb, A);
+        w.hi = load_window<CC>(bits, lay, bb, A - 64);
+    }
+    __device__ __forceinline__ void end_block(int) const {}
+    __device__ __forceinline__ void window(const Win& w, int b, int j, unsigned& win, int& dd) const {
+        (void)b;
+        const int lane = lane_id();
+        const int d = uniform(w.A - j);  // 0 .. 96
+        if (d <= 31) {
+            win = (w.A - lane >= 1) ? w.lo : 0u;
+            dd = d;
+        } else {
+            const int o = d + lane;  // column w.A - o
+            const unsigned a = (unsigned)__shfl((int)w.lo, o & 63);
+            const unsigned h = (unsigned)__shfl((int)w.hi, o & 63);
+            win = (w.A - o >= 1 && o < 128) ? (o < 64 ? a : h) : 0u;
+            dd = 0;
+        }
+    }
+};
+
+// Decision words recomputed from checkpoint rows (MODE 2 kernels).  The backtrack test at
+// (t, j) is the forward's comparison `tr[t-1, j-1] + em[t-1, tok[j-1]] > tr[t-1, j] + em[t-1,
+// blank]` (alignment.py:372-378, :400-404), and fp32 adds and maxima are deterministic, so the
+// forward's decisions are recomputed bit for bit from the row it started the chunk with.  A
+// block's path enters at column j and leaves at >= j - 32, so its words are needed for columns
+// j - 32 .. j; over 32 steps a cell depends on the 32 cells to its left, so the band is the
+// 64 lanes L -> column j - 63 + L started from checkpoint row 32b plus column j - 64 as lane 0's
+// first left input: lane L's decision at step k is exact when L >= k (lane 0's later left
+// inputs are unknown), i.e. columns >= j - 32 at every step.  Column 0 (tr[t][0], :367-370)
+// is not a cell: where the band reaches it, its lane is set every step from the fp64 cumsum
+// (checkpointed per chunk) in the reference's order.
+//
+// The block's 32 emission rows are staged per wave into an LDS slot ([32][VS], row stride VS
+// so the per-step reads take immediate offsets) by LDS-DMA.  A walker with two slots (one-wave
+// kernels: the forward's two buffers) loads the next block's rows into the other slot while it
+// computes; one slot per walker (multi-wave kernels) loads its rows at use and warms the L2
+// with the next block's rows (a DMA into a shared scratch row nobody reads).  The checkpoint
+// values and token ids of the window are loaded with the walk's three-block prefetch (columns
+// A - lane, A - 64 - lane, A - 128 - lane: the band of a block entered within 96 columns of A).
+template <int CC, int VS>
+struct CkSrc {
+    const float* ck;      // checkpoint rows: tr[32q][j] at cell j's bitmap word of block q
+    Layout lay;
+    const double* acc;    // [q]: sum of em[0 .. 32q - 1, 0] in fp64 (column 0 before row 32q)
+    const float* E;       // segment's emission rows [T, V]
+    const int32_t* tok;   // segment's tokens
+    int T, N, V, blank;
+    bool x4;              // V == 32 and 16-byte aligned rows: 8 rows per DMA instruction
+    float* slot[2];       // LDS [kChunk][VS] slots of this wave (slot[1] == slot[0]: one slot)
+    float* junk;          // LDS: 1 KB the L2 warm-up DMA writes
+    int cur = 0, rdy_blk = -1000;  // slot holding block rdy_blk's rows, landed
+    struct Win {
+        float c0, c1, c2;  // checkpoint row of block bb: columns A - lane, A - 64 - lane, A - 128 - lane
+        int k0, k1, k2;    // token ids of the same columns
+        int A;
+    };
+    __device__ __forceinline__ float ck_of(const float* row, int col) const {
+        col = max(col, 1);  // (columns <= 0: a don't-care lane)
+        int g, k;
+        lay.locate<CC>(col - 1, g, k);
+        return row[(unsigned)(k * lay.lanes + g)];
+    }
+    __device__ __forceinline__ int tok_of(int col) const { return tok[max(col, 1) - 1]; }
+    __device__ __forceinline__ void issue(Win& w, int bb, int A) const {
+        w.A = uniform(A);
+        const int lane = lane_id();
+        const int bc = uniform(max(bb, 0));
+        const float* row = ck + (int64_t)bc * (lay.C * lay.lanes);
+        w.c0 = ck_of(row, A - lane);
+        w.c1 = ck_of(row, A - 64 - lane);
+        w.c2 = ck_of(row, A - 128 - lane);
+        w.k0 = tok_of(A - lane);
+        w.k1 = tok_of(A - 64 - lane);
+        w.k2 = tok_of(A - 128 - lane);
+    }
+    // LDS-DMA of block b's rows (clamped into the segment) to dst, or all onto the junk row
+    __device__ __forceinline__ void dma_rows(int b, float* dst, bool warm) const {
+        const int l = lane_id();
+        const int r0 = max(b, 0) * kChunk;
+        const unsigned base = (unsigned)uniform((int)lds_addr(warm ? junk : dst));
+        if (VS == 32 && x4) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = min(r0 + 8 * i + (l >> 3), T - 1);
+                glds_dwordx4(E, (unsigned)(r * 32 + (l & 7) * 4) * 4u, base + (warm ? 0u : (unsigned)(i * 1024)));
+            }
+        } else if (l < V) {
+            for (int r = 0; r < kChunk; ++r) {
+                const int t = min(r0 + r, T - 1);
+                glds_dword(E + (int64_t)t * V, (unsigned)l * 4u, base + (warm ? 0u : (unsigned)(r * VS * 4)));
+            }
+        }
+    }
+    // The slot holding block b's rows.  Two slots: block b - 1's rows go into the other slot now
+    // and are waited for at the end of block b (end_block), a block later.  One slot: the L2 is
+    // warmed with block b - 1's rows now; end_block loads them into the slot once block b's
+    // recompute has read it.  (Waiting for a DMA here would also wait for the window loads the
+    // walk issued at the end of the previous block: an HBM round trip per block.)
+    __device__ __forceinline__ const float* stage(int b) {
+        const bool two = slot[1] != slot[0];
+        if (uniform(rdy_blk) != b) {  // (the first block, or after a jump)
+            cur = 0;
+            dma_rows(b, slot[0], false);
+            wait_vm();
+            rdy_blk = b;
+        }
+        const float* s = cur ? slot[1] : slot[0];  // (no dynamic index: it would put the struct in scratch)
+        if (two)
+            dma_rows(b - 1, cur ? slot[0] : slot[1], false);
+        else
+            dma_rows(b - 1, nullptr, true);
+        return s;
+    }
+    // block b walked: the next block's rows ready before the walk issues its next window loads
+    __device__ __forceinline__ void end_block(int b) {
+        if (slot[1] != slot[0]) {
+            wait_vm();
+            cur ^= 1;
+        } else {
+            dma_rows(b - 1, slot[0], false);
+            wait_vm();
+        }
+        rdy_blk = b - 1;
+    }
+    __device__ __forceinline__ void window(const Win& w, int b, int j, unsigned& win, int& dd) {
+        const int lane = lane_id();
+        const int d = uniform(w.A - j);  // 0 .. 96
+        const float* slotp = stage(b);
+        // band lane L: column j - 63 + L, at window offset o = d + 63 - L
+        const int o = d + 63 - lane;
+        const float x0 = __shfl(w.c0, o & 63), x1 = __shfl(w.c1, o & 63), x2 = __shfl(w.c2, o & 63);
+        const int y0 = __shfl(w.k0, o & 63), y1 = __shfl(w.k1, o & 63), y2 = __shfl(w.k2, o & 63);
+        float v = o < 64 ? x0 : (o < 128 ? x1 : x2);
+        int tk = o < 64 ? y0 : (o < 128 ? y1 : y2);
+        tk = (tk >= 0 && tk < V) ? tk : 0;
+        const int o0 = d + 64;  // column j - 64: lane 0's first left input
+        // (column 0 when j == 64: not a checkpointed cell)
+        const float left0 = j == 64 ? col0_value(b * kChunk, acc[max(b, 0)], T, N)
+                                    : uniformf(o0 < 128 ? __shfl(w.c1, o0 & 63) : __shfl(w.c2, o0 & 63));
+        const char* sb = reinterpret_cast<const char*>(slotp);
+        const int toff = tk * 4, boff = blank * 4;
+        unsigned bits = 0u;
+        // 32 steps in groups of four, the next group's LDS operands read ahead (sched_barrier
+        // keeps hipcc from hoisting all the reads: registers are the forward's occupancy).
+        // HAS_C0: column 0 is band lane 63 - j (j <= 63), set every step from the cumsum.
+        auto steps = [&](auto has_c0_tag) {
+            constexpr bool HAS_C0 = decltype(has_c0_tag)::value;
+            const bool c0 = HAS_C0 && lane == 63 - j;
+            double a = HAS_C0 ? acc[max(b, 0)] : 0.0;  // (rare: a load in the chain is fine)
+            const int t0 = b * kChunk;
+            if (c0) v = col0_value(t0, a, T, N);
+            float eb[4], et[4], e0[4];
+            auto rd = [&](int k0, float(&xb)[4], float(&xt)[4], float(&x0)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    xb[u] = *reinterpret_cast<const float*>(sb + boff + (k0 + u) * VS * 4);
+                    xt[u] = *reinterpret_cast<const float*>(sb + toff + (k0 + u) * VS * 4);
+                    if (HAS_C0) x0[u] = *reinterpret_cast<const float*>(sb + (k0 + u) * VS * 4);
+                }
+            };
+            rd(0, eb, et, e0);
+#pragma unroll
+            for (int g = 0; g < kChunk / 4; ++g) {
+                float nb[4], nt[4], n0[4];
+                if (g + 1 < kChunk / 4) rd(4 * (g + 1), nb, nt, n0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = 4 * g + u;
+                    const float left = k == 0 ? dpp_shr1(left0, v)
+                                              : __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                                                              __builtin_bit_cast(int, v), 0x138 /* wave_shr:1 */,
+                                                                              0xF, 0xF, true));
+                    const float st = v + eb[u];
+                    const float ch = left + et[u];
+                    bits = shift_in(bits, ch, st);
+                    v = nan_max(st, ch);
+                    if constexpr (HAS_C0) {
+                        a += (double)e0[u];
+                        if (c0) v = col0_value(t0 + k + 1, a, T, N);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    eb[u] = nb[u];
+                    et[u] = nt[u];
+                    if (HAS_C0) e0[u] = n0[u];
+                }
+            }
+        };
+        if (j > 63)
+            steps(BoolTag<false>{});
+        else
+            steps(BoolTag<true>{});
+        // lane i of the walk's window = column j - i = band lane 63 - i
+        const unsigned r = (unsigned)__shfl((int)bits, 63 - lane);
+        win = (j - lane >= 1) ? r : 0u;
+        dd = 0;
+    }
+};
+
 struct SpecWalk {
     int K, L, L0, top;  // segments; blocks per segment (segment 0: L0)
     const int* colrec;  // LDS, per block: the segment walker's column after it (-1: not reached)
@@ -1739,14 +2001,16 @@ struct SpecWalk {
 // path moves at most 32 columns per block, so block b - 3 starts at most 64 columns left of
 // A and ends within 128 of it.  At use, the 64 lanes from the walk's offset are gathered
 // into one word per lane (two ds_bpermutes, skipped while the block fits the first word).
-template <class LoadWin>  // LoadWin(b, A): this lane's word of column A - lane in block b (clamped)
-__device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsigned first_mask, int b_stop,
+//
+// Src is where the decision words come from: BitSrc reads the forward's bitmap, CkSrc (the
+// checkpointed throughput kernels) recomputes each block's band from the forward's checkpoint
+// rows.  Src::issue(w, bb, A) starts block bb's loads for a walk standing at column A;
+// Src::window(w, b, j, win, dd) makes win = the block's words with lane dd + i = column j - i.
+template <class Src>
+__device__ __forceinline__ int walk_range(Src& src, int j, int b, unsigned first_mask, int b_stop,
                                           unsigned* cmask, bool cmask_in_lds, int* colrec, const SpecWalk* spec,
                                           int& j_out, int wtop = 0x7fffffff, int* jentry = nullptr) {
-    struct Win {
-        unsigned lo, hi;
-        int A;
-    };
+    using Win = typename Src::Win;
     typedef __attribute__((address_space(3))) int lds_int;
     const int lane = lane_id();
     b = uniform(b);
@@ -1777,27 +2041,13 @@ __device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsi
         }
         gtop = 63;
     };
-    auto issue = [&](Win& w, int bb, int A) {
-        w.A = uniform(A);
-        w.lo = load_win(bb, A);
-        w.hi = load_win(bb, A - 64);
-    };
+    auto issue = [&](Win& w, int bb, int A) { src.issue(w, bb, A); };
     // walks block b with window w (wn, wa: the next two blocks' windows, re-issued after a
     // jump); false when the walk is over (result in res)
     auto block = [&](Win& w, Win& wn, Win& wa, int& res) -> bool {
-        const int d = uniform(w.A - j);  // 0 .. 96
         unsigned win;
         int dd;
-        if (d <= 31) {
-            win = (w.A - lane >= 1) ? w.lo : 0u;
-            dd = d;
-        } else {
-            const int o = d + lane;  // column w.A - o
-            const unsigned a = (unsigned)__shfl((int)w.lo, o & 63);
-            const unsigned h = (unsigned)__shfl((int)w.hi, o & 63);
-            win = (w.A - o >= 1 && o < 128) ? (o < 64 ? a : h) : 0u;
-            dd = 0;
-        }
+        src.window(w, b, j, win, dd);
         win &= first_mask;
         first_mask = 0xFFFFFFFFu;
         const int d0 = dd;
@@ -1859,6 +2109,7 @@ __device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsi
             }
         }
         if (done || (b & 63) == 0) flush(b);
+        src.end_block(b);
         issue(w, b - 3, j);  // unconditional (a conditional refill would merge and wait)
         if (done) {
             res = r;
@@ -1881,18 +2132,19 @@ __device__ __forceinline__ int walk_range(LoadWin&& load_win, int j, int b, unsi
     }
 }
 
-template <class LoadWin>
-__device__ __forceinline__ int walk_impl(LoadWin&& load_win, int N, int t_start, unsigned* cmask, bool cmask_in_lds) {
+template <class Src>
+__device__ __forceinline__ int walk_impl(Src& src, int N, int t_start, unsigned* cmask, bool cmask_in_lds) {
     if (t_start <= 0 || N <= 0) return -1;
     int jo;
-    return walk_range(load_win, N, (t_start - 1) >> 5, 0xFFFFFFFFu << (31 - ((t_start - 1) & 31)), 0, cmask,
+    return walk_range(src, N, (t_start - 1) >> 5, 0xFFFFFFFFu << (31 - ((t_start - 1) & 31)), 0, cmask,
                       cmask_in_lds, nullptr, nullptr, jo);
 }
 
 template <int CC>  // cells per lane of the bitmap layout (0: runtime lay.C)
 __device__ int walk(const unsigned* __restrict__ bits, const Layout& lay, int N, int t_start, unsigned* cmask,
                     bool cmask_in_lds) {
-    return walk_impl([&](int b, int A) { return load_window<CC>(bits, lay, b, A); }, N, t_start, cmask, cmask_in_lds);
+    BitSrc<CC> src{bits, lay};
+    return walk_impl(src, N, t_start, cmask, cmask_in_lds);
 }
 
 // Speculative walk: blocks top..0 of a walk from (t_start, N) in K segments over the workgroup's
@@ -1907,10 +2159,11 @@ constexpr int kSpecMinBlocks = 4;  // blocks per segment at least
 constexpr int kSpecOverlap = 2;  // unrecorded blocks a walker starts above its segment (A/B: 1, 3, 4 slower)
 // wave 0's t_start search, in walk blocks (A/B: 1, 3 or 5 within noise)
 constexpr int kSpecArgmaxBlocks = 3;
-template <int CC>
-__device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, int N, int T, const float* cn,
-                         int* argred, unsigned* cmask, int K, int* colrec, int* sbuf, int& t_start) {
-    auto lw = [&](int b, int A) { return load_window<CC>(bits, lay, b, A); };
+template <class Src>
+__device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn, unsigned* cmask, bool cmask_in_lds,
+                                         int K, int* colrec, int* sbuf, int& t_start) {
+    // (one walk_range call site before the barrier and one after: every call site inlines a
+    // copy of the walk, and the checkpointed walk's blocks are long)
     const int wv = uniform((int)threadIdx.x >> 6);
     const int lane = lane_id();
     SpecWalk sw;
@@ -1923,36 +2176,55 @@ __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, i
     unsigned fm = 0u;
     // The segments cover the blocks below T (t_start <= T): the walkers start while wave 0
     // alone finds t_start, so its segment is kSpecArgmaxBlocks shorter than theirs.  (Round 2
-    // waited for a workgroup-wide t_start first: 1-2 us slower.)
+    // waited for a workgroup-wide t_start first: 1-2 us slower.)  K == 1: wave 0 walks alone.
     sw.top = (T - 1) >> 5;
     sw.L = max((sw.top + 1 + kSpecArgmaxBlocks + K - 1) / K, 1);
     sw.L0 = max(sw.L - kSpecArgmaxBlocks, 1);
     while (K > 1 && sw.lo(K - 2) == 0) --K;  // (segments past block 0 would be empty)
+    if (K == 1) sw.L0 = sw.top + 1;
     sw.K = K;
     sw.sres = sbuf + K;
     sw.send = sbuf + 2 * K;
     const int tref = T;
-    if (wv == 0) t_start = column_argmax(cn, T);
+    // this wave's first walk: wave 0 the top segment from (t_start, N); wave k < K its segment
+    // from a guessed column kSpecOverlap blocks above it
+    bool go = false;
+    int j0 = N, b0 = 0, stop = 0, top = 0x7fffffff, je = -1;
+    unsigned fm0 = 0xFFFFFFFFu;
+    int* rec = nullptr;
     if (wv == 0) {
+        t_start = column_argmax(cn, T);
         if (t_start <= 0) {
             res = -1;  // (the reference's None)
         } else {
             tb = (t_start - 1) >> 5;
             fm = 0xFFFFFFFFu << (31 - ((t_start - 1) & 31));
-            res = tb >= sw.lo(0) ? walk_range(lw, N, tb, fm, sw.lo(0), cmask, true, nullptr, nullptr, jo)
-                                 : -3;  // starts in a lower segment: after the barrier
+            go = tb >= sw.lo(0);
+            res = -3;  // (starts in a lower segment: after the barrier)
+            b0 = tb;
+            fm0 = fm;
+            stop = sw.lo(0);
         }
     } else if (wv < K) {
-        const int top = sw.lo(wv - 1) - 1, lo = sw.lo(wv), sb = top + kSpecOverlap;
+        top = sw.lo(wv - 1) - 1;
+        const int lo = sw.lo(wv), sb = top + kSpecOverlap;
         // guess: the straight line from (0, 0) to (tref, N), inside the cells the path can
         // occupy at time 32 (sb + 1) (column <= time, N - column <= remaining steps)
         const int tt = 32 * (sb + 1);
         int g = (int)(((int64_t)N * tt + tref / 2) / tref);
         g = min(max(g, max(1, N - (tref - tt))), min(N, tt));
         for (int bb = lo + lane; bb <= top; bb += kWave) colrec[bb] = -1;
-        int je = -1;  // column entering the segment (-1: the path ended above it)
-        const int r = walk_range(lw, g, sb, 0xFFFFFFFFu, lo, cmask, true, colrec, nullptr, jo, top, &je);
-        if (lane == 0) {
+        go = true;
+        j0 = g;
+        b0 = sb;
+        stop = lo;
+        rec = colrec;
+    }
+    if (go) {
+        const int r = walk_range(lw, j0, b0, fm0, stop, cmask, cmask_in_lds, rec, nullptr, jo, top, &je);
+        if (wv == 0) {
+            res = r;
+        } else if (lane == 0) {  // je: column entering the segment (-1: the path ended above it)
             sbuf[wv] = je;
             sbuf[K + wv] = r;
             sbuf[2 * K + wv] = jo;
@@ -1960,17 +2232,22 @@ __device__ int walk_spec(const unsigned* __restrict__ bits, const Layout& lay, i
     }
     wave_fence();
     block_fence();
-    if (wv == 0 && res == -2) {
-        // segments entered on their guessed column are the true walk's as a whole
-        int k = 1;
-        for (; k < K && jo == uniform(sbuf[k]); ++k) {
-            res = uniform(sbuf[K + k]);
-            jo = uniform(sbuf[2 * K + k]);
-            if (res != -2) return res;
+    if (wv == 0 && (res == -2 || res == -3)) {
+        int j1 = N, b1 = tb;
+        unsigned fm1 = fm;
+        if (res == -2) {
+            // segments entered on their guessed column are the true walk's as a whole
+            int k = 1;
+            for (; k < K && jo == uniform(sbuf[k]); ++k) {
+                res = uniform(sbuf[K + k]);
+                jo = uniform(sbuf[2 * K + k]);
+                if (res != -2) return res;
+            }
+            j1 = jo;
+            b1 = sw.lo(k - 1) - 1;
+            fm1 = 0xFFFFFFFFu;
         }
-        res = walk_range(lw, jo, sw.lo(k - 1) - 1, 0xFFFFFFFFu, 0, cmask, true, nullptr, &sw, jo);
-    } else if (wv == 0 && res == -3) {
-        res = walk_range(lw, N, tb, fm, 0, cmask, true, nullptr, &sw, jo);
+        res = walk_range(lw, j1, b1, fm1, 0, cmask, cmask_in_lds, nullptr, &sw, jo);
     }
     return res;
 }
@@ -2020,6 +2297,53 @@ __device__ void merge_tokens(const float* __restrict__ E, int V, const int32_t* 
             for (int u = 0; u < 8; ++u) sum += (double)v[u];
         }
         for (; x < e; ++x) sum += (double)q0[x];
+        seg_end[k] = e;
+        seg_score[k] = sum / (double)(e - s);
+    }
+}
+
+// merge_tokens with the segment's q0 row and start frames staged in LDS first (coalesced, 8
+// loads in flight per thread), so each token's left-to-right fp64 sum reads LDS instead of
+// a chain of dependent global loads; each token's first-frame emission is loaded one token
+// ahead.  Needs T + N floats of `lds`; every thread of the workgroup calls it.
+__device__ void merge_tokens_lds(const float* __restrict__ E, int V, const int32_t* __restrict__ tok, int N, int T,
+                                 int t_start, const float* __restrict__ q0, const int32_t* __restrict__ start,
+                                 int32_t* __restrict__ seg_end, double* __restrict__ seg_score, float* lds) {
+    float* qs = lds;
+    int* ss = reinterpret_cast<int*>(lds + T);
+    const int tid = (int)threadIdx.x, nthr = (int)blockDim.x;
+    constexpr int kB = 8;
+    for (int base = tid; base < T; base += kB * nthr) {
+        float v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = q0[min(base + u * nthr, T - 1)];
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (base + u * nthr < T) qs[base + u * nthr] = v[u];
+    }
+    for (int base = tid; base < N; base += kB * nthr) {
+        int v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) v[u] = start[min(base + u * nthr, N - 1)];
+#pragma unroll
+        for (int u = 0; u < kB; ++u)
+            if (base + u * nthr < N) ss[base + u * nthr] = v[u];
+    }
+    block_fence();
+    auto first = [&](int k) {  // em[start_k, tok_k] (clamped: an unconditional load)
+        const int kk = min(k, N - 1);
+        int tk = tok[kk];
+        tk = (tk >= 0 && tk < V) ? tk : 0;
+        return E[(int64_t)ss[kk] * V + tk];
+    };
+    float e_next = first(tid);
+    for (int k = tid; k < N; k += nthr) {
+        const float e_cur = e_next;
+        e_next = first(k + nthr);
+        const int s = ss[k];
+        const int e = (k + 1 < N) ? ss[k + 1] : t_start;
+        double sum = (double)exp_cr(e_cur);
+        for (int x = s + 1; x < e; ++x) sum += (double)qs[x];
         seg_end[k] = e;
         seg_score[k] = sum / (double)(e - s);
     }
@@ -2123,6 +2447,7 @@ struct AlignArgs {
     int bits_stride_cells;  // 64 * Cstride dwords per block
     float* q0;       // workspace: sum_T floats
     unsigned* cmask; // workspace: walk change masks, (floor(row0/32) + seg) words per segment
+    double* c0acc;   // workspace (MODE 2): column-0 fp64 cumsum per chunk, same offsets as cmask
     float* cn;       // workspace: column N history, segment at (row0 + 4 seg) & ~3
     int parts;       // split launches: workgroups (CUs) per segment, else 1
     int split_id;    // split launches: the one split bucket (segments up to its capacity)
@@ -2182,16 +2507,33 @@ __device__ __forceinline__ bool prepare_colmap(ColMapLds<VS>& m, ColMap& cm, con
     return cm.n <= kGatherVS;
 }
 
+// Row slots of the checkpointed walk (CkSrc), [kChunk][VS] each: two per walker wave (the next
+// block's rows load while a block computes) where that keeps the LDS of a workgroup within its
+// share at 4 waves per SIMD (VS == 32, and the one-wave kernels' two forward buffers), else one
+// per walker wave (rows loaded at use, the next block's warmed into the L2).
+template <int VS, int W>
+constexpr int kCkSlots =
+#ifdef WX_CK1
+    W == 1 ? 2 : W;
+#else
+    (W == 1 || VS == 32) ? 2 * W : W;
+#endif
+
 template <int C, int VS, int W, int H, bool SP = false>
 __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
+    // Checkpointed forward (MODE 2, CkSrc walk): the single-CU throughput kernels with two or
+    // more waves (speculative walkers) and staged row widths; the one-wave (a lone walker would
+    // recompute every block serially: slower than the bits it saves), latency (helper), split
+    // and gathered-vocabulary kernels keep the bitmap.
+    constexpr bool CK = !SP && H == 0 && VS != kGatherVS && W >= 2;
+    // (CK: the walkers' row slots, one [32][VS] per wave, reuse the forward's buffers)
     constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 4 * kChunk * VS ? kLatencyLdsFloats : 4 * kChunk * VS)
-                                 : 2 * kChunk * VS;
+                                 : (CK ? kCkSlots<VS, W> : 2) * kChunk * VS;
     __shared__ float lds[kLdsFloats];
-    __shared__ __attribute__((aligned(16))) float c0b[H ? 2 * kChunk : 1];
-    __shared__ float xh[W > 1 ? 2 * W * kWave : 1];
+    __shared__ __attribute__((aligned(16))) float c0b[H || (CK && W >= 2) ? 2 * kChunk : 1];
+    __shared__ __attribute__((aligned(16))) float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
-    __shared__ int argred[3 * (W + H)];
     __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
     __shared__ int sbuf_lds[3 * (W + H)];
     __shared__ ColMapLds<VS> cml;
@@ -2225,6 +2567,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     unsigned* bits = a.bits + ((d.row0 >> 5) + seg) * (int64_t)a.bits_stride_cells;
     float* q0 = a.q0 + d.row0;
     float* cn = a.cn + ((d.row0 + kCnPad * (int64_t)seg) & ~(int64_t)3);
+    double* c0acc = a.c0acc + ((d.row0 >> 5) + seg);
     WX_STAMP_RT(4);
     WX_STAMP(0);
     Split sp;
@@ -2243,8 +2586,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if (SP && lane == 0) tsb[2] = 0;
     bool lost = false;
     if (!slow)
-        lost = Forward<C, VS, 0, W, H != 0, SP, (H > 1 ? 2 : 1)>::run(d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh,
-                                                     a.x4 != 0, cm, nullptr, &sp);
+        lost = Forward<C, VS, CK ? 2 : 0, W, H != 0, SP, (H > 1 ? 2 : 1)>::run(
+            d, E, a.V, a.tok, bits, q0, cn, nullptr, lds, c0b, xh, a.x4 != 0, cm, nullptr, &sp, c0acc);
     WX_STAMP(1);
     if (SP && lost) tsb[2] = 1;  // (any lane of the consumer or, register-resident kernels, the poller)
     wait_vm();
@@ -2291,26 +2634,27 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
 #ifdef WX_PHASE_TIMING
     WX_T(w0);
 #endif
-    // t_start: with every wave when the workgroup has several (the walk waits for it)
-    // several waves: the walk's blocks in speculative segments, one per wave (walk_spec, which
-    // also finds t_start)
+    // t_start, the walk and the change masks: several waves walk speculative segments, one per
+    // wave (walk_spec, which also finds t_start); one wave walks alone
     const int nbw = ((d.T - 1) >> 5) + 1;
-    const int K = (W + H > 1 && d.T <= kMaxLdsFrames && d.N > 0) ? min(W + H, nbw / kSpecMinBlocks) : 1;
-    const int ts_block = (W + H > 1 && K < 2) ? block_argmax(cn, d.T, argred) : 0;
+    const bool lds_walk = d.T <= kMaxLdsFrames;
+    const int K = lds_walk ? max(1, min(W + H, nbw / kSpecMinBlocks)) : 1;
 #ifdef WX_PHASE_TIMING
     WX_T(w1);
 #endif
-    int ts_spec = 0;
-    const int b_lo_spec =
-        K >= 2 ? walk_spec<C>(bits, lay, d.N, d.T, cn, argred, cmask_lds, K, colrec_lds, sbuf_lds, ts_spec) : -1;
+    auto walk_tail = [&](auto& wsrc) {
+    int ts = 0, b_lo = -1;
+    unsigned* cmask = lds_walk ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
+    if constexpr (W + H > 1) b_lo = walk_spec(wsrc, d.N, d.T, cn, cmask, lds_walk, K, colrec_lds, sbuf_lds, ts);
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
-        const int ts = K >= 2 ? ts_spec : (W + H > 1) ? ts_block : column_argmax(cn, d.T);
+        if constexpr (W + H == 1) {
+            ts = column_argmax(cn, d.T);
+            b_lo = walk_impl(wsrc, d.N, ts, cmask, lds_walk);
+        }
         if (lane == 0) {
             a.t_start[seg] = ts;
             tsb[0] = ts;
         }
-        unsigned* cmask = (d.T <= kMaxLdsFrames) ? cmask_lds : a.cmask + ((d.row0 >> 5) + seg);
-        const int b_lo = K >= 2 ? b_lo_spec : walk<C>(bits, lay, d.N, ts, cmask, d.T <= kMaxLdsFrames);
 #ifdef WX_PHASE_TIMING
         WX_T(w2);
 #endif
@@ -2331,6 +2675,28 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     } else {
         if (H && !slow && !failed) fill_q0(E, a.V, d.T, q0, kWave);
     }
+    };
+    if constexpr (CK) {
+        CkSrc<C, VS> wsrc;
+        wsrc.ck = reinterpret_cast<const float*>(bits);
+        wsrc.lay = lay;
+        wsrc.acc = c0acc;
+        wsrc.E = E;
+        wsrc.tok = a.tok + d.tok0;
+        wsrc.T = d.T;
+        wsrc.N = d.N;
+        wsrc.V = a.V;
+        wsrc.blank = d.blank;  // (as the forward reads it)
+        wsrc.x4 = a.x4 != 0;
+        // one-wave kernels: both forward buffers are the walker's two slots; else one per wave
+        wsrc.slot[0] = lds + uniform((int)threadIdx.x >> 6) * kChunk * VS;
+        wsrc.slot[1] = kCkSlots<VS, W> >= 2 * W ? wsrc.slot[0] + W * kChunk * VS : wsrc.slot[0];
+        wsrc.junk = xh;  // (the forward's halo exchange, free now: 2 W 64 floats >= 1 KB when W > 1)
+        walk_tail(wsrc);
+    } else {
+        BitSrc<C> wsrc{bits, lay};
+        walk_tail(wsrc);
+    }
     wait_vm();
     block_fence();
     const int ts = tsb[0];
@@ -2339,13 +2705,16 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // low bits: 0 aligned / 1 None; flags: which segments took the generic forward
     if (lane == 0) a.status[seg] = (ok ? 0 : 1) | (failed ? WX_STATUS_RECOVERED : 0) | (slow ? WX_STATUS_GENERIC : 0);
     if (!ok) return;
-    merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
+    if (d.T + d.N <= kLdsFloats)
+        merge_tokens_lds(E, a.V, a.tok + d.tok0, d.N, d.T, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0, lds);
+    else
+        merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
     WX_STAMP(3);
     WX_STAMP_RT(5);
 }
 
 template <int C, int VS, int W, int H>
-__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(1, H ? 2 : 8))) void align_dp_kernel(
+__global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(H || VS == kGatherVS || C > 8 || W == 1 ? 1 : 4, H ? 2 : 8))) void align_dp_kernel(
     AlignArgs a) {
     align_dp_body<C, VS, W, H>(a);
 }
