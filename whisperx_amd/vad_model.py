@@ -262,7 +262,8 @@ def _shared_sinc_ok(model, w: torch.Tensor, hop: int) -> bool:
     if not isinstance(wn, torch.nn.InstanceNorm1d) or wn.num_features != 1 or (wn.track_running_stats and not wn.training):
         return False
     pool, norm = sn.pool1d[0], sn.norm1d[0]
-    probe = torch.empty((1, 80, 3), device=w.device).transpose(1, 2).contiguous().transpose(1, 2)
+    C = int(enc.weight().shape[0])  # the checkpoint's filter count (the probe's channels)
+    probe = torch.empty((1, C, 3), device=w.device).transpose(1, 2).contiguous().transpose(1, 2)
     return _fused_epilogue(pool, norm, probe)
 
 
@@ -394,7 +395,8 @@ class VoiceActivitySegmentation:
 
         Windows overlap tenfold (5 s every 0.5 s), and the filterbank is a bias-free strided
         convolution, so window b's stage-1 convolution is rows [b * hop / 10, + 7975) of the
-        convolution of the whole span.  The waveform InstanceNorm of the window (pyannote's
+        convolution of the whole span (computed per batch of windows: that batch's span).  The
+        waveform InstanceNorm of the window (pyannote's
         `wav_norm1d`) is an affine of its input — (x - mean_b) / std_b * g + h — and commutes
         into the convolution: conv(x_norm)[t, c] = (g / std_b) conv(x)[t, c] + (h - g mean_b /
         std_b) * sum(filter c).  wx_sincnet_stage_ex applies that per-window affine while it
@@ -406,8 +408,6 @@ class VoiceActivitySegmentation:
         wf = enc.weight()  # [80, 1, k]
         C, _, k = wf.shape
         s = enc.stride
-        span = (n_full - 1) * hop + win
-        G = _conv_global(w[0, :span], wf.reshape(C, k), s)  # [F, C] time-major
         L1 = (win - k) // s + 1
         fpw = hop // s
         # the windows' waveform statistics (InstanceNorm1d: biased variance, eps), in fp64
@@ -426,7 +426,12 @@ class VoiceActivitySegmentation:
         outs = []
         for i in range(0, n_full, self.batch_size):
             B = min(self.batch_size, n_full - i)
-            x1 = G.as_strided((B, L1, C), (fpw * C, C, 1), G.storage_offset() + i * fpw * C)
+            # the batch's span only: [frames, C] time-major, ~50 MB per 2,048 windows (the whole
+            # file's would be ~1.8 GB per hour); hop is a multiple of the stride, so the span's
+            # rows are the whole-waveform convolution's rows from window i on
+            span = (B - 1) * hop + win
+            G = _conv_global(w[0, i * hop:i * hop + span], wf.reshape(C, k), s)
+            x1 = G.as_strided((B, L1, C), (fpw * C, C, 1), G.storage_offset())
             y1 = _lib.sincnet_stage(x1, True, norm0.weight, norm0.bias, norm0.eps, in_scale=scale[i:i + B],
                                     in_shift=shift[i:i + B])
             outs.append(self.model.head(sn.stages(y1.transpose(1, 2), 1)))
