@@ -217,6 +217,36 @@ def test_align_dp_speculative_walk_skewed_paths(mode):
     _check_vs_oracle(_skewed_cases(np.random.default_rng(7)), f"skewed mode {mode}", mode)
 
 
+def test_align_dp_speculative_walk_trimmed_segments():
+    """walk_spec drops speculative segments that would start past block 0 (too few blocks for
+    the wave count).  With 8-wave workgroups that happens for T in 993-1024, 1185-1248 and
+    1441-1472 frames (the segment lengths are computed host-side below, as the kernel does);
+    those segments, in the one-CU latency buckets (1, 7, 1) and (2, 7, 1), equal the oracle,
+    random and tie-quantised."""
+    from whisperx_amd import _lib
+
+    def trimmed(T, nw=8):
+        top = (T - 1) >> 5
+        K = min(nw, (top + 1) // 4)
+        L = max((top + 1 + 3 + K - 1) // K, 1)
+        L0 = max(L - 3, 1)
+        lo = lambda k: max(top - L0 - k * L + 1, 0)
+        return K > 1 and lo(K - 2) == 0
+
+    rng = np.random.default_rng(99)
+    Ts = (993, 1010, 1024, 1185, 1200, 1248, 1441, 1472)
+    assert all(trimmed(T) for T in Ts) and not trimmed(992) and not trimmed(1473)
+    for quant in (None, 4):
+        cases = []
+        for T in Ts:
+            for N in (200, 600):
+                cases += _random_cases(rng, 1, (T, T + 1), (N, N + 1), 32, quant=quant)
+        plan = _lib.align_dp_plan(len(cases), 200, 600, 32, 2)
+        assert plan == ["void wx::align_dp_kernel<1, 32, 7, 1>(wx::AlignArgs)",
+                        "void wx::align_dp_kernel<2, 32, 7, 1>(wx::AlignArgs)"], plan
+        _check_vs_oracle(cases, f"trimmed walk segments quant={quant}", mode=2)
+
+
 def _capacity(C, W):
     """Tokens a (C cells/lane, W waves) bucket holds: waves >= 1 give ceil(32/C) lanes to the
     chunk halo (wx_align.hip, Geometry)."""

@@ -139,9 +139,14 @@ def child(args):
         med = float(np.median(ms))
         res = [x.cpu().numpy() for x in p.run()]
         torch.cuda.synchronize()
-        digest = [int(np.int64(hash(r.tobytes()) & 0x7FFFFFFF)) for r in res]
+        # results (starts, ends, scores, t_start, and the outcome bits of the status) apart from
+        # the route flags (recovered hand-off / generic forward): a recovered hand-off changes
+        # the route, never the result, and the two must be told apart
+        outcome = res[4] & _lib.STATUS_MASK
+        digest = [int(np.int64(hash(r.tobytes()) & 0x7FFFFFFF)) for r in res[:4] + [outcome]]
         out[case] = {"ms_med": med, "ms_min": float(min(ms)), "cells_per_s": cells / (med / 1e3),
-                     "GBps": Bytes / (med / 1e3) / 1e9, "frac": Bytes / (med / 1e3) / 8e12, "digest": digest}
+                     "GBps": Bytes / (med / 1e3) / 1e9, "frac": Bytes / (med / 1e3) / 8e12, "digest": digest,
+                     "status": _lib.status_summary(res[4][: b.S])}
         if args.phases:
             import ctypes
             lib = _lib.load()
@@ -260,10 +265,15 @@ def main():
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)
     libs = list(results)
+    for lib in libs:
+        for case, v in results[lib].items():
+            st = v.get("status", {})
+            if st.get("recovered_segments") or st.get("generic_forward_segments") or st.get("not_computed"):
+                print(f"ROUTE {lib} {case}: {st}", flush=True)
     for lib in libs[1:]:
         for case in results[lib]:
             if results[lib][case]["digest"] != results[libs[0]][case]["digest"]:
-                print(f"MISMATCH {lib} {case} vs {libs[0]}", flush=True)
+                print(f"RESULT MISMATCH {lib} {case} vs {libs[0]}", flush=True)
 
 
 if __name__ == "__main__":

@@ -2705,7 +2705,8 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // low bits: 0 aligned / 1 None; flags: which segments took the generic forward
     if (lane == 0) a.status[seg] = (ok ? 0 : 1) | (failed ? WX_STATUS_RECOVERED : 0) | (slow ? WX_STATUS_GENERIC : 0);
     if (!ok) return;
-    if (d.T + d.N <= kLdsFloats)
+    // (staging costs one more round trip: it pays when every thread has several tokens)
+    if (d.T + d.N <= kLdsFloats && d.N > 2 * (int)blockDim.x)
         merge_tokens_lds(E, a.V, a.tok + d.tok0, d.N, d.T, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0, lds);
     else
         merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
