@@ -15,6 +15,8 @@
  *                        the kernel under vad.py:264 merge_chunks
  *   wx_channel_norm   <- whisperx/alignment.py:226-233 (wav2vec2 forward: feature encoder's
  *                        GroupNorm + GELU, time-major)
+ *   wx_conv0_channel_norm <- the same layer with its 1-channel convolution fused (one pass
+ *                        over the output)
  *   wx_attention_f32  <- whisperx/alignment.py:226-233 (wav2vec2 forward: the encoder's
  *                        self-attention, fp32)
  *   wx_vad_aggregate  <- whisperx/vad.py:198-240 VoiceActivitySegmentation.apply's
@@ -217,6 +219,19 @@ int wx_binarize_plan(float onset, float offset, int64_t total_frames, char* buf,
 size_t wx_channel_norm_workspace_bytes(int32_t C);
 int wx_channel_norm(const float* x, int64_t L, int32_t C, const float* gamma, const float* beta, float eps,
                     int32_t gelu, float* y, void* workspace, size_t workspace_bytes, void* stream);
+
+/* wav2vec2's first feature-encoder layer (alignment.py:226-233, the emission forward; HF
+ * Wav2Vec2GroupNormConvLayer): y[t, c] = act(GroupNorm_c(conv(x)[t, c])) with conv a 1-input-
+ * channel Conv1d (K <= 16 taps, stride; w [C, K], bias [C] or NULL) over the S samples of x,
+ * GroupNorm with one group per channel (statistics over time in fp64, biased variance, affine
+ * gamma / beta, eps) and act the exact erf GELU when gelu != 0 (identity otherwise).  y is
+ * [Lout, C] time-major, Lout = (S - K) / stride + 1.  The convolution is recomputed in the
+ * second pass instead of being stored.  Equal to torch's conv + GroupNorm + GELU to fp32
+ * tolerance (its own summation order). */
+size_t wx_conv0_channel_norm_workspace_bytes(int64_t L, int32_t C);
+int wx_conv0_channel_norm(const float* x, int64_t S, int32_t K, int32_t stride, const float* w, const float* bias,
+                          int32_t C, const float* gamma, const float* beta, float eps, int32_t gelu, float* y,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* wav2vec2 self-attention (alignment.py:226-233, the emission forward's encoder layers):
  * o[b, t, h, :] = softmax(scale * q[b, h, t, :] . k[b, h, :, :]^T) v[b, h, :, :], fp32, no mask,

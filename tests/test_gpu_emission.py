@@ -38,6 +38,34 @@ def test_channel_norm_vs_torch_groupnorm(L, C, gelu):
     assert torch.equal(inplace, got)
 
 
+@pytest.mark.parametrize("S,K,stride,bias,gelu", [(480000, 10, 5, False, True), (112123, 10, 5, True, True),
+                                                  (400, 10, 5, False, False), (15, 10, 5, False, True),
+                                                  (3001, 16, 3, True, True), (64, 1, 1, False, True)])
+def test_conv0_channel_norm_vs_torch(S, K, stride, bias, gelu):
+    """wx_conv0_channel_norm (the feature encoder's first layer in one pass) against torch's fp32
+    Conv1d(1, 512, K, stride) -> GroupNorm(512, 512) -> GELU(erf), time-major: 30 s, 7 s, the
+    400-sample minimum, two frames, other tap counts / strides, with and without a conv
+    bias and the GELU."""
+    from whisperx_amd import _lib
+
+    torch.manual_seed(S)
+    C = 512
+    conv = torch.nn.Conv1d(1, C, K, stride=stride, bias=bias).cuda().eval()
+    gn = torch.nn.GroupNorm(C, C).cuda().eval()
+    with torch.no_grad():
+        gn.weight.copy_(torch.randn(C) * 0.5 + 1)
+        gn.bias.copy_(torch.randn(C) * 0.1)
+    x = (torch.randn(S, device="cuda") * 0.1).contiguous()
+    with torch.no_grad():
+        ref = gn(conv(x[None, None]))
+        if gelu:
+            ref = torch.nn.functional.gelu(ref)
+        ref = ref[0].t()  # [Lout, C]
+        got = _lib.conv0_channel_norm(x, conv.weight, conv.bias, stride, gn.weight, gn.bias, gn.eps, gelu)
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=5e-5, atol=5e-5)
+
+
 @pytest.mark.parametrize("shape", [(1, 1499, 768), (2, 97, 1024), (1, 1, 768), (3, 5, 256), (1, 0, 512)])
 def test_add_layernorm_vs_torch(shape):
     """wx_add_layernorm against torch's fp32 `layer_norm(a + b)` (the encoder layer's residual

@@ -76,6 +76,9 @@ SIGNATURES = {
     "wx_align_dp_plan": (ctypes.c_int, [_i32, _i64, _i64, _i32, _i32, ctypes.c_char_p, _sz]),
     "wx_channel_norm_workspace_bytes": (_sz, [_i32]),
     "wx_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _f32, _i32, _vp, _vp, _sz, _vp]),
+    "wx_conv0_channel_norm_workspace_bytes": (_sz, [_i64, _i32]),
+    "wx_conv0_channel_norm": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _f32, _i32, _vp, _vp,
+                                             _sz, _vp]),
     "wx_add_layernorm": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _vp, _f32, _vp, _vp, _vp]),
     "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
@@ -570,6 +573,27 @@ def channel_norm(x: torch.Tensor, gamma, beta, eps: float, gelu: bool, out: Opti
     with torch.cuda.device(x.device):
         _check(lib.wx_channel_norm(_ptr(x), L, C, _ptr(gamma), _ptr(beta), float(eps), int(bool(gelu)), _ptr(y),
                                    _ptr(ws), ws.numel(), ctypes.c_void_p(stream.cuda_stream)))
+    return y
+
+
+def conv0_channel_norm(x: torch.Tensor, w: torch.Tensor, bias, stride: int, gamma, beta, eps: float, gelu: bool,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """wx_conv0_channel_norm: the 1-channel conv (w [C, 1, K] or [C, K]) over the samples x [S]
+    (contiguous fp32 device tensor), GroupNorm per channel, GELU; returns [Lout, C] time-major."""
+    lib = load()
+    S = int(x.shape[-1])
+    C, K = int(w.shape[0]), int(w.shape[-1])
+    w2 = w.reshape(C, K).contiguous()
+    L = (S - K) // stride + 1 if S >= K else 0
+    y = out if out is not None else torch.empty((L, C), dtype=torch.float32, device=x.device)
+    if L == 0:
+        return y
+    stream = torch.cuda.current_stream(x.device)
+    ws = _ws_emit.get(f"{x.device}/{stream.cuda_stream}/c0", lib.wx_conv0_channel_norm_workspace_bytes(L, C), x.device)
+    with torch.cuda.device(x.device):
+        _check(lib.wx_conv0_channel_norm(_ptr(x), S, K, int(stride), _ptr(w2), _ptr(bias) if bias is not None else None,
+                                         C, _ptr(gamma), _ptr(beta), float(eps), int(bool(gelu)), _ptr(y), _ptr(ws),
+                                         ws.numel(), ctypes.c_void_p(stream.cuda_stream)))
     return y
 
 

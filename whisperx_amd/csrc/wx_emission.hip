@@ -88,6 +88,135 @@ __global__ __launch_bounds__(256) void chan_apply_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------
+// The feature encoder's first layer as one pass over its output: conv (1 input channel, k taps,
+// stride s: wav2vec2's 512 x 10 / 5) -> GroupNorm(one group per channel, over time) -> exact
+// GELU, time-major [Lout, C].  Through the GEMM route this layer was a bias fill, a K = 10 GEMM
+// writing 196 MB per 30 s segment (~12 TFLOP/s: HBM-bound on its own output), and the three
+// channel-norm kernels reading it back twice (~230 us).  Here pass 1 computes the convolution in
+// registers and reduces per-channel fp64 (sum, sum of squares) without writing it; pass 2
+// recomputes it (k multiply-adds per value, cheaper than reading it back) and writes
+// gelu(v * a[c] + b[c]) once.  A thread owns one channel (its k weights in registers) over
+// kC0Rows consecutive rows; a wave covers 64 consecutive channels, so every row's store is 256
+// contiguous bytes and the k waveform samples of a row are the same for the whole wave.
+constexpr int kC0Rows = 16;  // rows per thread
+constexpr int kC0MaxK = 16;  // taps held in registers
+
+template <int K>
+__device__ __forceinline__ float conv0_at(const float* __restrict__ x, int64_t t, int stride, const float (&w)[K],
+                                          float bias) {
+    const float* xr = x + t * stride;
+    float v = bias;
+#pragma unroll
+    for (int j = 0; j < K; ++j) v = v + xr[j] * w[j];  // (-ffp-contract=off: separate multiply and add)
+    return v;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void conv0_stats_kernel(const float* __restrict__ x, int64_t L, int stride,
+                                                          const float* __restrict__ wt, const float* __restrict__ bias,
+                                                          int C, double* __restrict__ part /* [nblk][2][C] */) {
+    const int c = blockIdx.x * kCols + (threadIdx.x & (kCols - 1));
+    const int wv = threadIdx.x / kCols;
+    float w[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = c < C ? wt[(int64_t)c * K + j] : 0.f;
+    const float b = (bias && c < C) ? bias[c] : 0.f;
+    const int64_t t0 = ((int64_t)blockIdx.y * kRows + wv) * kC0Rows;
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < kC0Rows; ++r) {
+        const int64_t t = t0 + r;
+        if (t >= L) break;
+        const double v = (double)conv0_at<K>(x, t, stride, w, b);
+        s += v;
+        q += v * v;
+    }
+    __shared__ double ss[kRows][kCols], qq[kRows][kCols];
+    ss[wv][threadIdx.x & (kCols - 1)] = s;
+    qq[wv][threadIdx.x & (kCols - 1)] = q;
+    __syncthreads();
+    if (wv == 0 && c < C) {
+        for (int r = 1; r < kRows; ++r) {
+            s += ss[r][threadIdx.x];
+            q += qq[r][threadIdx.x];
+        }
+        part[(int64_t)blockIdx.y * 2 * C + c] = s;
+        part[(int64_t)blockIdx.y * 2 * C + C + c] = q;
+    }
+}
+
+// (a, b) per channel from nblk partials: 4 row groups per channel tile sum a quarter each with
+// 8 loads in flight, combined in group order
+__global__ __launch_bounds__(256) void conv0_finish_kernel(const double* __restrict__ part, int nblk, int64_t L, int C,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           float eps, float* __restrict__ ab) {
+    const int c = blockIdx.x * kCols + (threadIdx.x & (kCols - 1));
+    const int g = threadIdx.x / kCols;
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+        const int lo = g * nblk / kRows, hi = (g + 1) * nblk / kRows;
+        int k = lo;
+        for (; k + 8 <= hi; k += 8) {
+            double vs[8], vq[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                vs[u] = part[(int64_t)(k + u) * 2 * C + c];
+                vq[u] = part[(int64_t)(k + u) * 2 * C + C + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s += vs[u];
+                q += vq[u];
+            }
+        }
+        for (; k < hi; ++k) {
+            s += part[(int64_t)k * 2 * C + c];
+            q += part[(int64_t)k * 2 * C + C + c];
+        }
+    }
+    __shared__ double ss[kRows][kCols], qq[kRows][kCols];
+    ss[g][threadIdx.x & (kCols - 1)] = s;
+    qq[g][threadIdx.x & (kCols - 1)] = q;
+    __syncthreads();
+    if (g != 0 || c >= C) return;
+    for (int r = 1; r < kRows; ++r) {
+        s += ss[r][threadIdx.x];
+        q += qq[r][threadIdx.x];
+    }
+    const double mean = s / (double)L;
+    const double var = fmax(q / (double)L - mean * mean, 0.0);  // biased, as GroupNorm
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    const double gg = gamma ? (double)gamma[c] : 1.0, bb = beta ? (double)beta[c] : 0.0;
+    ab[c] = (float)(rstd * gg);
+    ab[C + c] = (float)(bb - mean * rstd * gg);
+}
+
+__device__ __forceinline__ float gelu_erf0(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+
+template <int K>
+__global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restrict__ x, int64_t L, int stride,
+                                                          const float* __restrict__ wt, const float* __restrict__ bias,
+                                                          int C, const float* __restrict__ ab, int gelu,
+                                                          float* __restrict__ y) {
+    const int c = blockIdx.x * kCols + (threadIdx.x & (kCols - 1));
+    const int wv = threadIdx.x / kCols;
+    if (c >= C) return;
+    float w[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = wt[(int64_t)c * K + j];
+    const float b = bias ? bias[c] : 0.f;
+    const float sa = ab[c], sb = ab[C + c];
+    const int64_t t0 = ((int64_t)blockIdx.y * kRows + wv) * kC0Rows;
+#pragma unroll 4
+    for (int r = 0; r < kC0Rows; ++r) {
+        const int64_t t = t0 + r;
+        if (t >= L) break;
+        float v = conv0_at<K>(x, t, stride, w, b) * sa + sb;
+        if (gelu) v = gelu_erf0(v);
+        y[t * C + c] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // wav2vec2 self-attention, fp32 (alignment.py:226-233: the encoder's 12 / 24 attention layers,
 // one unpadded segment per forward, no mask).  torch's fused attention kernel for fp32
 // (aotriton attn_fwd) took 34% of config 3's GPU time at ~26 TFLOP/s (profiles/
@@ -362,6 +491,43 @@ extern "C" int wx_channel_norm(const float* x, int64_t L, int32_t C, const float
     const int64_t n4 = L * (C / 4);
     hipLaunchKernelGGL(chan_apply_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, x, n4, C / 4, ab, C,
                        gelu, y);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" size_t wx_conv0_channel_norm_workspace_bytes(int64_t L, int32_t C) {
+    if (L <= 0 || C <= 0) return 0;
+    const int64_t nblk = (L + wxe::kRows * wxe::kC0Rows - 1) / (wxe::kRows * wxe::kC0Rows);
+    return (size_t)nblk * 2 * C * sizeof(double) + 2 * (size_t)C * sizeof(float);
+}
+
+extern "C" int wx_conv0_channel_norm(const float* x, int64_t S, int32_t K, int32_t stride, const float* w,
+                                     const float* bias, int32_t C, const float* gamma, const float* beta, float eps,
+                                     int32_t gelu, float* y, void* workspace, size_t workspace_bytes, void* stream) {
+    using namespace wxe;
+    if (S < 0 || C <= 0 || K < 1 || K > kC0MaxK || stride < 1 || !x || !w || !y) return WX_E_INVALID;
+    const int64_t L = S >= K ? (S - K) / stride + 1 : 0;
+    if (L == 0) return WX_OK;
+    if (!workspace || workspace_bytes < wx_conv0_channel_norm_workspace_bytes(L, C)) return WX_E_WORKSPACE;
+    const int64_t nblk = (L + kRows * kC0Rows - 1) / (kRows * kC0Rows);
+    if (nblk > 65535) return WX_E_INVALID;  // (grid y; ~4.2 h of 16 kHz audio at stride 5)
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    double* part = reinterpret_cast<double*>(workspace);
+    float* ab = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
+    const dim3 grid((C + kCols - 1) / kCols, (unsigned)nblk), blk(kCols * kRows);
+#define WX_C0(KK)                                                                                              \
+    case KK:                                                                                                   \
+        hipLaunchKernelGGL(conv0_stats_kernel<KK>, grid, blk, 0, st, x, L, stride, w, bias, C, part);           \
+        hipLaunchKernelGGL(conv0_finish_kernel, dim3((C + kCols - 1) / kCols), blk, 0, st, part, (int)nblk, L, C, \
+                           gamma, beta, eps, ab);                                                              \
+        hipLaunchKernelGGL(conv0_apply_kernel<KK>, grid, blk, 0, st, x, L, stride, w, bias, C, ab, gelu, y);    \
+        break;
+    switch (K) {
+        WX_C0(1) WX_C0(2) WX_C0(3) WX_C0(4) WX_C0(5) WX_C0(6) WX_C0(7) WX_C0(8) WX_C0(9) WX_C0(10) WX_C0(11)
+        WX_C0(12) WX_C0(13) WX_C0(14) WX_C0(15) WX_C0(16)
+        default: return WX_E_INVALID;
+    }
+#undef WX_C0
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

@@ -190,15 +190,32 @@ def _is_erf_gelu(act) -> bool:
 
 def _patched_gn_layer(self, x):
     """conv -> GroupNorm(one group per channel) -> activation (HF Wav2Vec2GroupNormConvLayer,
-    the feature encoder's first layer) on time-major activations: the GEMM conv, then
-    wx_channel_norm with the erf GELU fused (one HBM read for statistics, one read + write)."""
+    the feature encoder's first layer) on time-major activations: for its 1-channel conv, all
+    three in wx_conv0_channel_norm (the conv recomputed per pass, the output written once);
+    otherwise the GEMM conv, then wx_channel_norm with the erf GELU fused (one HBM read for
+    statistics, one read + write)."""
     if not (x.is_cuda and not torch.is_grad_enabled() and x.dim() == 3):
         return self._wx_orig_forward(x)
     from . import _lib
 
     gn = self.layer_norm
-    y = _conv1d_gemm(self.conv, x).transpose(1, 2)  # [B, L, C] contiguous (time-major)
     gelu = _is_erf_gelu(self.activation)
+    conv = self.conv
+    (k,) = conv.kernel_size
+    if (not os.environ.get("WX_NO_CONV0_FUSED") and conv.in_channels == 1 and conv.groups == 1
+            and conv.dilation == (1,) and not isinstance(conv.padding, str) and conv.padding == (0,)
+            and gn.num_groups == conv.out_channels and k <= 16 and x.dtype == torch.float32):
+        # conv + GroupNorm + GELU in one pass over the output (wx_conv0_channel_norm): the K = 10
+        # GEMM's 196 MB output is never written and read back
+        w = _weight(conv)
+        (s_,) = conv.stride
+        L = (x.shape[-1] - k) // s_ + 1
+        y = torch.empty((x.shape[0], max(L, 0), conv.out_channels), dtype=x.dtype, device=x.device)
+        for b in range(x.shape[0]):
+            _lib.conv0_channel_norm(x[b, 0].contiguous(), w, conv.bias, s_, gn.weight, gn.bias, gn.eps, gelu, out=y[b])
+        out = y.transpose(1, 2)
+        return out if gelu else self.activation(out)
+    y = _conv1d_gemm(self.conv, x).transpose(1, 2)  # [B, L, C] contiguous (time-major)
     for b in range(y.shape[0]):
         _lib.channel_norm(y[b], gn.weight, gn.bias, gn.eps, gelu, out=y[b])
     out = y.transpose(1, 2)
