@@ -243,6 +243,18 @@ int wx_attention_f32(const float* q, const float* k, const float* v, float* o, i
                      int32_t D, const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides,
                      float scale, void* stream);
 
+/* The same attention over nseg segments packed back to back in one launch (the emission
+ * producer's packed encoder: every segment's rows in one [rows, H, 64] batch, each segment
+ * attending only to itself — the reference's one-unpadded-forward-per-segment semantics,
+ * alignment.py:217-233).  seg_rows (device, nseg + 1): segment s owns rows [seg_rows[s],
+ * seg_rows[s + 1]); seg_units (device, nseg + 1): prefix of H * ceil(T_s / 32), n_units its
+ * last entry.  q/k/v element strides {head, row} (*_strides[0..1]); o [rows, H, 64] contiguous.
+ * split: waves per 32-query tile (1, 2 or 4; 0 = chosen from n_units). */
+int wx_attention_f32_packed(const float* q, const float* k, const float* v, float* o, int32_t nseg,
+                            const int32_t* seg_rows, const int32_t* seg_units, int32_t n_units, int32_t H, int32_t D,
+                            const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides, float scale,
+                            int32_t split, void* stream);
+
 /* wav2vec2 encoder layer's residual add + LayerNorm (alignment.py:226-233, the emission
  * forward: `layer_norm(residual + x)` twice per layer): for each of `rows` rows of D floats
  * (D in {256, 512, 768, 1024}; row strides a_stride / b_stride elements, multiples of 4; all

@@ -106,6 +106,97 @@ def test_attention_f32_vs_fp64(B, H, T):
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("split", [0, 1, 2, 4])
+def test_attention_f32_packed_vs_fp64(split):
+    """wx_attention_f32_packed: ragged segments packed by rows (lengths 1499, 37, 1, 0, 500, 64,
+    33, 2999, as transformers' views of one fused [rows, 3 x H x 64] q/k/v projection), each
+    segment attending only to its own rows, against a per-segment fp64 attention; every
+    wave split, and the automatic choice."""
+    from whisperx_amd import _lib
+
+    torch.manual_seed(11 + split)
+    H = 12
+    lengths = [1499, 37, 1, 0, 500, 64, 33, 2999]
+    segs = _lib.PackedSegments(lengths)
+    R = segs.rows
+    qkv = torch.randn(1, R, 3 * H * 64, device="cuda") * 2
+    q, k, v = (qkv[..., i * H * 64:(i + 1) * H * 64].view(1, R, H, 64).transpose(1, 2) for i in range(3))
+    got = _lib.attention_f32_packed(q, k, v, 0.125, segs, split)  # [1, R, H, 64]
+    assert got.shape == (1, R, H, 64)
+    for a, b in zip(segs.offsets[:-1], segs.offsets[1:]):
+        if b == a:
+            continue
+        qd, kd, vd = (x[:, :, a:b].double() for x in (q, k, v))
+        ref = (torch.softmax(qd @ kd.transpose(-1, -2) * 0.125, -1) @ vd).transpose(1, 2).float()
+        torch.testing.assert_close(got[:, a:b], ref, rtol=1e-5, atol=2e-5, msg=f"segment rows [{a}, {b})")
+
+
+def _packed_vs_per_segment(m, V, lengths, tol=5e-5):
+    """emission.packed_logits over ragged waveforms against the stock per-segment forward."""
+    from whisperx_amd import _lib, alignment, emission
+
+    rng = np.random.default_rng(sum(lengths))
+    wavs = [torch.from_numpy(rng.standard_normal(n).astype(np.float32) * 0.1)[None].cuda() for n in lengths]
+    with torch.inference_mode():
+        ref = [torch.log_softmax(m(w if w.shape[-1] >= 400 else torch.nn.functional.pad(w, (0, 400 - w.shape[-1]))).logits,
+                                 -1)[0] for w in wavs]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    worst = 0.0
+    with emission.prepared(m):
+        emission.materialize_weights(m)
+        assert emission.packed_supported(m)
+        Ts = [emission.n_frames(n, m) for n in lengths]
+        with torch.inference_mode():
+            got = torch.log_softmax(emission.packed_logits(m, wavs, _lib.PackedSegments(Ts), streams), -1)
+        torch.cuda.synchronize()
+        # and through _emissions (pack ranges, CSR rows, events)
+        csr = alignment._emissions(m, "huggingface", wavs, "cuda:0", n_streams=3)
+        main = torch.cuda.current_stream()
+        for st in csr.streams:
+            main.wait_stream(st)
+        torch.cuda.synchronize()
+    off = np.cumsum([0] + Ts)
+    for i, r in enumerate(ref):
+        g = got[off[i]: off[i + 1]]
+        assert g.shape == r.shape, (i, g.shape, r.shape)
+        err = float((g - r).abs().max())
+        worst = max(worst, err)
+        assert err <= tol, f"segment {i} ({lengths[i]} samples): max |packed - stock| = {err}"
+        assert torch.equal(g.argmax(-1), r.argmax(-1)), f"segment {i}: frame argmax differs"
+        assert torch.equal(csr[i], g), f"segment {i}: _emissions differs from packed_logits"
+    return worst
+
+
+@pytest.mark.parametrize("fe", ["packed", "per_segment"])
+def test_packed_encoder_matches_stock_base(fe, monkeypatch):
+    """The packed encoder (all segments' rows in one transformer pass, attention per segment)
+    on wav2vec2-base: 30 s, a < 400-sample segment (padded like alignment.py:217-224), 7.3 s,
+    the 400-sample minimum and 1 s — each segment's log-probabilities equal its own stock
+    forward's to fp32 tolerance with identical frame argmax.  The feature encoder either packed
+    too (one GEMM per tap over the aligned sample buffer) or run per segment."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    if fe == "per_segment":
+        monkeypatch.setenv("WX_NO_PACKED_FE", "1")
+    torch.manual_seed(21)
+    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
+    worst = _packed_vs_per_segment(m, 32, [30 * 16000, 250, int(7.3 * 16000), 400, 16000])
+    print(f"base packed vs stock: max |dlogp| = {worst:.3g}")
+
+
+def test_packed_encoder_matches_stock_large_xlsr():
+    """The same on the stable-layer-norm / layer-norm-feature-encoder family (8 layers of
+    large-xlsr's width to keep the test short)."""
+    from transformers import Wav2Vec2ForCTC
+
+    torch.manual_seed(22)
+    cfg = large_xlsr_config()
+    cfg.num_hidden_layers = 8
+    m = Wav2Vec2ForCTC(cfg).cuda().eval()
+    worst = _packed_vs_per_segment(m, 40, [int(12.5 * 16000), 16000 + 7, 60 * 16000])
+    print(f"large-xlsr packed vs stock: max |dlogp| = {worst:.3g}")
+
+
 def _check_prepared_vs_stock(m, V, lengths, tol=5e-5):
     from whisperx_amd import emission
 
@@ -165,7 +256,9 @@ def test_emissions_fan_out_fresh_parametrised_model():
     built model the cache must exist before the forwards fan out over 8 streams, or the
     streams read it before it is computed.  Segment 0 is much longer than the others (its
     stream would still be building the weight when the others reach the positional conv).
-    Every segment's emission must equal a single-stream forward of the same model to 1e-6."""
+    Every segment's emission must equal a single-stream forward of the same model (to 1e-6
+    through the per-segment route; to fp32 tolerance through the packed encoder, whose GEMMs
+    tile differently)."""
     from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
 
     from whisperx_amd import alignment, emission
@@ -186,7 +279,8 @@ def test_emissions_fan_out_fresh_parametrised_model():
         for i, w in enumerate(wavs):
             ref = torch.log_softmax(m(w).logits, -1)[0]
             err = float((csr[i] - ref).abs().max())
-            assert err <= 1e-6, f"segment {i}: fan-out emission differs from single-stream by {err}"
+            tol = 5e-5 if emission.packed_supported(m) else 1e-6
+            assert err <= tol, f"segment {i}: fan-out emission differs from single-stream by {err}"
             assert torch.equal(csr[i].argmax(-1), ref.argmax(-1))
     emission.restore_model(m)
 

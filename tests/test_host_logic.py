@@ -54,3 +54,82 @@ def test_interpolate_nans_list_and_series():
         assert interpolate_nans(pd.Series(vals), m).tolist() == ref
     assert interpolate_nans([float("nan"), 2.0], "nearest") == [2.0, 2.0]
     assert interpolate_nans([1.0, 2.0], "nearest") == [1.0, 2.0]
+
+
+def test_pack_ranges():
+    """The packed encoder's segment ranges: consecutive, at most `cap` frames each, a longer
+    segment alone."""
+    from whisperx_amd import alignment
+
+    assert alignment._pack_ranges([], 10) == []
+    assert alignment._pack_ranges([4, 4, 4], 10) == [(0, 2), (2, 3)]
+    assert alignment._pack_ranges([12, 1, 9, 1], 10) == [(0, 1), (1, 3), (3, 4)]
+    assert alignment._pack_ranges([5, 5], 10) == [(0, 2)]
+    # a last pack of >= 4 segments leaves its last quarter to a pack of its own
+    assert alignment._pack_ranges([1499] * 16, 49152) == [(0, 12), (12, 16)]
+    assert alignment._pack_ranges([1] * 9, 6) == [(0, 6), (6, 9)]
+    assert alignment._pack_ranges([1] * 10, 6) == [(0, 6), (6, 9), (9, 10)]
+
+
+def test_packed_segments_layout():
+    from whisperx_amd import _lib
+
+    s = _lib.PackedSegments([3, 0, 40])
+    assert s.offsets == [0, 3, 3, 43] and s.rows == 43
+
+
+def test_round3_matches_python_round():
+    """alignment._round3 (vectorised char-timestamp rounding) equals Python's round(v, 3) on
+    random values, exact decimal ties, their neighbouring doubles and timestamp-like products."""
+    import math
+
+    import numpy as np
+
+    from whisperx_amd import alignment
+
+    rng = np.random.default_rng(3)
+    vals = list(rng.random(20000) * 7200) + list(rng.random(2000))
+    ties = [k / 1000 + 0.0005 for k in range(0, 200000, 7)]
+    vals += ties + [math.nextafter(v, 0) for v in ties] + [math.nextafter(v, 1e9) for v in ties]
+    vals += [int(f) * (30.0 / 1499) + 30.0 * s for f in range(1499) for s in (0, 7, 113)]
+    vals += [-v for v in vals[:500]] + [0.0, -0.0, 1e-9, 0.0005, 0.0015, 2.675]
+    x = np.array(vals, dtype=np.float64)
+    got = alignment._round3(x)
+    for v, g in zip(vals, got):
+        r = round(v, 3)
+        assert g == r and math.copysign(1, g) == math.copysign(1, r), (v, g, r)
+
+
+def test_nanmean_matches_numpy_sum():
+    import math
+
+    import numpy as np
+
+    from whisperx_amd import alignment
+
+    rng = np.random.default_rng(4)
+    for n in range(1, 20):
+        for _ in range(300):
+            vals = [round(float(v), 3) for v in rng.random(n)]
+            if n > 2:
+                vals[int(rng.integers(n))] = math.nan
+            cnt = sum(1 for v in vals if v == v)
+            ref = np.float64(np.array([v if v == v else 0.0 for v in vals]).sum() / cnt)
+            assert alignment._nanmean(vals) == ref
+
+
+def test_np_round3_matches_numpy_scalar_round():
+    import math
+
+    import numpy as np
+
+    from whisperx_amd import alignment
+
+    rng = np.random.default_rng(5)
+    vals = list(rng.random(20000)) + [k / 1000 + 0.0005 for k in range(3000)] + [2.675, 0.0005, -0.0004, -0.0, 0.0]
+    vals += [math.nan, math.inf, -math.inf, 1e300]
+    for v in vals:
+        ref = round(np.float64(v), 3)
+        got = alignment._np_round3(np.float64(v))
+        assert type(got) is type(ref)
+        assert (got == ref and math.copysign(1, got) == math.copysign(1, ref)) or (ref != ref and got != got), (v, got, ref)

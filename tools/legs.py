@@ -60,6 +60,12 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         print(f"e2e: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, {len(segs)} segments", flush=True)
+        from whisperx_amd import alignment
+
+        if alignment.PHASE_TIMES:  # WX_PROFILE=1: per-phase wall time (synchronised phases)
+            n = a.steps + max(1, a.warmup)
+            print("phases (ms per launch): " + ", ".join(f"{k} {1000 * v / n:.2f}"
+                                                        for k, v in alignment.PHASE_TIMES.items()), flush=True)
         return
     if a.leg == "cfg2":
         ems, toks = make_batch(64, 1499, 32, 300, 500, 1000, dev)

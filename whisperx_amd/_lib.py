@@ -83,6 +83,8 @@ SIGNATURES = {
     "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
+    "wx_attention_f32_packed": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
+                                               _f32, _i32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
                                    _vp, _vp, _vp, _vp, _vp]),
     "wx_binarize_workspace_bytes": (_sz, [_i32, _i64]),
@@ -633,6 +635,56 @@ def attention_f32(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: floa
     with torch.cuda.device(q.device):
         _check(lib.wx_attention_f32(_ptr(q), _ptr(k), _ptr(v), _ptr(o), B, H, T, D, st[0], st[1], st[2],
                                     float(scale), _stream(q.device)))
+    return o
+
+
+class PackedSegments:
+    """Row layout of segments packed back to back (the packed encoder's batch): host lengths
+    and, per device, the int32 tables wx_attention_f32_packed reads — seg_rows (row offsets) and
+    seg_units (prefix of H x 32-query tiles), uploaded once per (device, H)."""
+
+    def __init__(self, lengths):
+        self.lengths = [int(t) for t in lengths]
+        self.offsets = [0]
+        for t in self.lengths:
+            self.offsets.append(self.offsets[-1] + t)
+        self.rows = self.offsets[-1]
+        self._dev = {}
+
+    def tables(self, device, H: int):
+        key = (str(device), int(H))
+        t = self._dev.get(key)
+        if t is None:
+            units = [0]
+            for n in self.lengths:
+                units.append(units[-1] + H * ((n + 31) // 32))
+            if units[-1] > 2 ** 31 - 1 or self.rows > 2 ** 31 - 1:
+                raise WXError("attention_f32_packed: more than 2^31 rows or work units")
+            host = torch.tensor(self.offsets + units, dtype=torch.int32).pin_memory()
+            dev = host.to(device, non_blocking=True)
+            n = len(self.lengths) + 1
+            t = (dev[:n], dev[n:], units[-1], host)  # (the pinned source lives as long as the copy)
+            self._dev[key] = t
+        return t
+
+
+def attention_f32_packed(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float, segs: PackedSegments,
+                         split: int = 0) -> torch.Tensor:
+    """wx_attention_f32_packed: per-segment softmax(scale * q k^T) v over segments packed along
+    the row axis of [1, H, rows, 64] fp32 device views (head dim contiguous).  Returns
+    [1, rows, H, 64] like attention_f32."""
+    lib = load()
+    B, H, R, D = (int(x) for x in q.shape)
+    if B != 1 or R != segs.rows or tuple(k.shape) != (1, H, R, D) or tuple(v.shape) != (1, H, R, D):
+        raise WXError(f"attention_f32_packed: q/k/v {tuple(q.shape)} / {tuple(k.shape)} / {tuple(v.shape)} "
+                      f"do not cover the {segs.rows} packed rows")
+    o = torch.empty((1, R, H, D), dtype=torch.float32, device=q.device)
+    rows_t, units_t, n_units, _ = segs.tables(q.device, H)
+    st = [(ctypes.c_int64 * 2)(int(t.stride(1)), int(t.stride(2))) for t in (q, k, v)]
+    with torch.cuda.device(q.device):
+        _check(lib.wx_attention_f32_packed(_ptr(q), _ptr(k), _ptr(v), _ptr(o), len(segs.lengths), _ptr(rows_t),
+                                           _ptr(units_t), n_units, H, D, st[0], st[1], st[2], float(scale), int(split),
+                                           _stream(q.device)))
     return o
 
 

@@ -25,6 +25,7 @@ There is no CPU fallback: without a HIP device the DP raises.
 """
 from __future__ import annotations
 
+import bisect
 import contextlib
 import math
 import os
@@ -248,6 +249,7 @@ class _EmissionsCSR:
             self.off.append(self.off[-1] + T)
         self.events = events  # per segment: recorded on its forward's stream after log_softmax
         self.streams = []
+        self.groups = None  # packed encoder: the packs' segment ranges
 
     def sub(self, a: int, b: int) -> "_EmissionsCSR":
         """Segments [a, b) as their own packed matrix (a row-range view: no copy)."""
@@ -256,8 +258,11 @@ class _EmissionsCSR:
 
     def wait(self, stream):
         """Make `stream` wait for these segments' forwards."""
+        seen = set()
         for ev in self.events or ():
-            stream.wait_event(ev)
+            if id(ev) not in seen:  # (a pack's segments share its event)
+                seen.add(id(ev))
+                stream.wait_event(ev)
 
     def __len__(self):
         return len(self.Ts)
@@ -311,10 +316,19 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     if streams is None:
         streams = [torch.cuda.Stream(device=dev) for _ in range(max(n_streams, 1))]
         _EMISSION_STREAMS[key] = streams
-    bad = False
-    csr.events = []
     for st in streams:
         st.wait_stream(main)
+    if model_type == "huggingface" and emission.packed_supported(model):
+        try:
+            csr.groups = _pack_ranges(Ts)
+            csr.events = _packed_emissions(model, waveforms, csr, streams)
+            csr.streams = streams
+            return csr
+        except ValueError:  # a model whose frame geometry is not n_frames': per-segment path
+            for st in streams:
+                st.wait_stream(main)
+    bad = False
+    csr.events = []
     for i, w in enumerate(waveforms):
         st = streams[i % len(streams)]
         with torch.cuda.stream(st):
@@ -335,6 +349,60 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     # joins every stream back onto the current one
     csr.streams = streams
     return csr
+
+
+_PACK_ROWS = 49152  # encoder rows per pack (~16 min of audio; WX_PACK_ROWS overrides)
+
+
+def _pack_ranges(Ts, cap: Optional[int] = None):
+    """Consecutive segment ranges [a, b) of at most `cap` frames each (a longer segment alone).
+    WX_PACK_PLAN="12,4" (development A/B): explicit segments per pack instead."""
+    plan = os.environ.get("WX_PACK_PLAN")
+    if plan and cap is None:
+        packs, a = [], 0
+        for k in (int(x) for x in plan.split(",")):
+            if a < len(Ts):
+                packs.append((a, min(len(Ts), a + k)))
+                a = packs[-1][1]
+        if a < len(Ts):
+            packs.append((a, len(Ts)))
+        return packs
+    cap = int(os.environ.get("WX_PACK_ROWS", _PACK_ROWS)) if cap is None else cap
+    packs, a, rows = [], 0, 0
+    for i, T in enumerate(Ts):
+        if i > a and rows + T > cap:
+            packs.append((a, i))
+            a, rows = i, 0
+        rows += T
+    if Ts:
+        packs.append((a, len(Ts)))
+    # the last pack's quarter as a pack of its own: the host aggregates the rest of it while
+    # the GPU runs that tail, leaving only the tail's aggregation after the last kernel
+    # (e2e_align, 16 x 30 s: one pack 85.6 ms, 12 + 4 84.6 ms, 8 + 8 86.9 ms)
+    a, b = packs[-1] if packs else (0, 0)
+    if b - a >= 4:
+        packs[-1:] = [(a, b - (b - a) // 4), (b - (b - a) // 4, b)]
+    return packs
+
+
+def _packed_emissions(model, waveforms, csr, streams):
+    """The packed-encoder route of _emissions (emission.packed_logits): segments in the packs
+    csr.groups (consecutive ranges, _pack_ranges), all on streams[0] (the others only serve
+    packed_logits' per-segment feature-encoder fallback), log_softmax of the whole pack into
+    its CSR rows.  Returns the per-segment events (a pack's segments share its event)."""
+    events = []
+    # every pack on one stream: pack p finishes (and its DP and host aggregation start) as
+    # early as possible instead of sharing the GPU with pack p + 1
+    ps = streams[0]
+    for a, b in csr.groups:
+        with torch.cuda.stream(ps):
+            lg = emission.packed_logits(model, waveforms[a:b], _lib.PackedSegments(csr.Ts[a:b]), streams)
+            with torch.inference_mode():
+                emission.log_softmax_into(lg, csr.em[csr.off[a]: csr.off[b]])
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        events += [ev] * (b - a)
+    return events
 
 
 def _dp_device(device):
@@ -381,49 +449,58 @@ def align(
     model_lang = align_model_metadata["language"]
     model_type = align_model_metadata["type"]
 
-    # 1. text preparation (mutates the input segments like the reference)
-    total_segments = len(transcript)
-    with _Phase("prepare"):
-        for sdx, segment in enumerate(transcript):
-            if print_progress:
-                base_progress = ((sdx + 1) / total_segments) * 100
-                percent_complete = (50 + base_progress / 2) if combined_progress else base_progress
-                print(f"Progress: {percent_complete:.2f}%...")
-            _prepare(segment, model_dictionary, model_lang)
-
-    # 2a. emissions for every alignable segment, queued on the device
+    # 2a. the emission forward of every segment that starts inside the audio, queued on the
+    # device first, so that the host prepares the transcripts (step 1) while the GPU runs them.
+    # A segment whose text has no alignable char wastes its forward: the reference skips it
+    # (alignment.py:185-195), and so do the DP and the aggregation below.
     blank_id = blank_id_of(model_dictionary)
     dp_dev = _dp_device(device)
     if torch.device(device).type == "cuda" and not audio.is_cuda:
         # one host->device copy of the waveform: per-segment copies from pageable memory would
         # each wait for their stream's earlier forwards, keeping the host in lock-step with them
         audio = audio.to(dp_dev)
-    plan = []  # per segment: ("skip", reason) | ("dp", index into batch)
-    ems, toks, blanks, meta = [], [], [], []
+    fwd_pos = {}  # transcript index -> index of its forward
+    wavs = []
     for sdx, segment in enumerate(transcript):
         t1, t2 = segment["start"], segment["end"]
-        if len(segment["clean_char"]) == 0:
-            plan.append(("nochars", None))
-            continue
         if t1 >= MAX_DURATION:
-            plan.append(("toolate", None))
             continue
-        text_clean = "".join(segment["clean_char"])
-        tokens = [model_dictionary[c] for c in text_clean]
-        f1 = int(t1 * SAMPLE_RATE)
-        f2 = int(t2 * SAMPLE_RATE)
-        waveform_segment = audio[:, f1:f2]
-        plan.append(("dp", len(ems)))
-        ems.append(waveform_segment)
-        toks.append(tokens)
-        blanks.append(blank_id)
-        meta.append((text_clean, waveform_segment.size(0)))
+        fwd_pos[sdx] = len(wavs)
+        wavs.append(audio[:, int(t1 * SAMPLE_RATE): int(t2 * SAMPLE_RATE)])
     # the model is prepared (GEMM convolutions, wx attention) for this call only: the caller's
     # model is restored when align() returns, after every forward has been joined
     gpu_route = torch.device(device).type == "cuda" and not os.environ.get("WX_MIOPEN_CONV")
     with emission.prepared(model) if gpu_route else contextlib.nullcontext():
         with _Phase("emission"):
-            ems = _emissions(model, model_type, ems, device)
+            ems = _emissions(model, model_type, wavs, device)
+
+        # 1. text preparation (mutates the input segments like the reference)
+        total_segments = len(transcript)
+        with _Phase("prepare"):
+            for sdx, segment in enumerate(transcript):
+                if print_progress:
+                    base_progress = ((sdx + 1) / total_segments) * 100
+                    percent_complete = (50 + base_progress / 2) if combined_progress else base_progress
+                    print(f"Progress: {percent_complete:.2f}%...")
+                _prepare(segment, model_dictionary, model_lang)
+
+        plan = []  # per segment: ("nochars" | "toolate", None) | ("dp", index of its forward)
+        dummy = [0 if blank_id != 0 else 1]  # (tokens of a forwarded segment the DP result of which is unused)
+        toks = [dummy] * len(wavs)
+        blanks = [blank_id] * len(wavs)
+        meta = [("", 1)] * len(wavs)
+        for sdx, segment in enumerate(transcript):
+            if len(segment["clean_char"]) == 0:
+                plan.append(("nochars", None))
+                continue
+            if segment["start"] >= MAX_DURATION:
+                plan.append(("toolate", None))
+                continue
+            i = fwd_pos[sdx]
+            text_clean = "".join(segment["clean_char"])
+            toks[i] = [model_dictionary[c] for c in text_clean]
+            meta[i] = (text_clean, wavs[i].size(0))
+            plan.append(("dp", i))
 
         # 2b. the fused DP, one launch per group of segments, and 2c. timestamps and aggregation
         # in segment order (same prints, same order).  A group's DP waits only for its own
@@ -478,13 +555,19 @@ class _GroupedDP:
     def __init__(self, ems, toks, blanks, dev, n_groups: int = 4, min_group: int = 8):
         self.ems, self.toks, self.blanks, self.dev = ems, toks, blanks, dev
         n = len(ems)
-        self.size = max(min_group, -(-n // n_groups)) if n else 1
         self.res = [None] * n
+        groups = getattr(ems, "groups", None)  # the packed encoder's packs: one DP per pack
+        if not groups:
+            size = max(min_group, -(-n // n_groups)) if n else 1
+            groups = [(a, min(n, a + size)) for a in range(0, n, size)]
+        self.group_of = [None] * n
+        for g in groups:
+            for i in range(g[0], g[1]):
+                self.group_of[i] = g
 
     def __getitem__(self, i):
         if self.res[i] is None:
-            a = (i // self.size) * self.size
-            b = min(len(self.res), a + self.size)
+            a, b = self.group_of[i]
             sub = self.ems.sub(a, b) if isinstance(self.ems, _EmissionsCSR) else self.ems[a:b]
             self.res[a:b] = _run_dp(sub, self.toks[a:b], self.blanks[a:b], self.dev)
         return self.res[i]
@@ -544,12 +627,52 @@ def _nanmax(vals):
 
 
 def _nanmean(vals):
-    """pandas Series.mean(): NaNs zeroed, numpy (pairwise) sum, / non-NaN count."""
+    """pandas Series.mean(): NaNs zeroed, numpy (pairwise) sum, / non-NaN count.  numpy sums
+    fewer than 8 float64 values sequentially from 0.0 (its pairwise sum's base case), which
+    the Python loop reproduces exactly without an array round trip."""
     cnt = sum(1 for v in vals if v == v)
     if cnt == 0:
         return np.float64(math.nan)
+    if len(vals) < 8:
+        s = 0.0
+        for v in vals:
+            if v == v:
+                s += v
+            else:
+                s += 0.0
+        return np.float64(s / cnt)
     arr = np.array([v if v == v else 0.0 for v in vals], dtype=np.float64)
     return np.float64(arr.sum() / cnt)
+
+
+def _np_round3(v):
+    """round(np.float64 v, 3) as numpy computes it (the reference rounds pandas' mean, a numpy
+    scalar: rint(v * 1000) / 1000, not Python's correctly rounded round) without numpy's
+    per-scalar overhead; Python's round(float) is round-half-even like rint."""
+    if v != v or v in (math.inf, -math.inf):
+        return np.float64(v)
+    y = float(v) * 1000.0
+    r = float(round(y))
+    if r == 0.0:
+        r = math.copysign(0.0, y)  # (rint keeps the sign of a zero)
+    return np.float64(r / 1000.0)
+
+
+def _round3(x: np.ndarray) -> list:
+    """[round(v, 3) for v in x] (Python's correctly rounded round) for a float64 array,
+    vectorised: rint(v * 1000) / 1000 is the same double (an exact integer over 1000,
+    correctly rounded by the division, as round's decimal -> double step) unless v * 1000 lies
+    within its rounding error of a half-integer, where the product may round across the tie;
+    those values go through round() itself."""
+    y = x * 1000.0
+    out = np.rint(y) / 1000.0
+    near = np.abs(y - np.floor(y) - 0.5) <= 1e-6
+    res = out.tolist()
+    if near.any():
+        xs = x.tolist()
+        for i in np.flatnonzero(near).tolist():
+            res[i] = round(xs[i], 3)
+    return res
 
 
 def aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang, interpolate_method,
@@ -559,25 +682,38 @@ def aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang, 
     t1, t2, text = segment["start"], segment["end"], segment["text"]
     duration = t2 - t1
     ratio = duration * n_channels / T
-    clean_pos = {cdx: i for i, cdx in enumerate(segment["clean_cdx"])}
     no_spaces = model_lang in LANGUAGES_WITHOUT_SPACES
     n = len(text)
-    c_start = [math.nan] * n
-    c_end = [math.nan] * n
-    c_score = [math.nan] * n
-    c_word = [0] * n
-    word_idx = 0
-    for cdx in range(n):
-        i = clean_pos.get(cdx)
-        if i is not None:
-            c_start[cdx] = round(int(starts[i]) * ratio + t1, 3)
-            c_end[cdx] = round(int(ends[i]) * ratio + t1, 3)
-            c_score[cdx] = round(float(scores[i]), 3)
-        c_word[cdx] = word_idx
-        if no_spaces:
-            word_idx += 1
-        elif cdx == n - 1 or text[cdx + 1] == " ":
-            word_idx += 1
+    cdx = segment["clean_cdx"]
+    if len(cdx):
+        # round(int(start) * ratio + t1, 3) etc. per clean char (the same double operations),
+        # NaN for the other chars
+        m = len(cdx)
+        ci = np.asarray(cdx, dtype=np.int64)
+        cols = []
+        for v in (np.asarray(starts[:m], dtype=np.int64).astype(np.float64) * ratio + t1,
+                  np.asarray(ends[:m], dtype=np.int64).astype(np.float64) * ratio + t1,
+                  np.asarray(scores[:m], dtype=np.float64)):
+            col = np.full(n, np.nan)
+            col[ci] = _round3(v)
+            cols.append(col.tolist())
+        c_start, c_end, c_score = cols
+    else:
+        c_start = [math.nan] * n
+        c_end = [math.nan] * n
+        c_score = [math.nan] * n
+    # words: the reference's word index advances after every char followed by a space (after
+    # every char for languages without spaces), so word k is the char run [wb[k], wb[k + 1]):
+    # it starts at 0 and at every space after position 0
+    if no_spaces:
+        wb = list(range(n + 1))
+    else:
+        wb = [0]
+        p = text.find(" ", 1)
+        while p != -1:
+            wb.append(p)
+            p = text.find(" ", p + 1)
+        wb.append(n)
 
     subs = []
     for (sstart, send) in segment["sentence_spans"]:
@@ -587,29 +723,25 @@ def aggregate_segment(segment, starts, ends, scores, T, n_channels, model_lang, 
         sentence_start = _nanmin(c_start[r] for r in rows)
         sentence_end = _nanmax(c_end[r] for r in rows if text[r] != " ")
         words = []
-        seen = {}
-        order = []
-        for r in rows:
-            w = c_word[r]
-            if w not in seen:
-                seen[w] = []
-                order.append(w)
-            seen[w].append(r)
-        for w in order:
-            idx = seen[w]
-            word_text = "".join(text[r] for r in idx).strip()
+        # the words meeting rows [lo, hi], each clipped to them, in order
+        k0 = bisect.bisect_right(wb, lo) - 1 if hi >= lo else len(wb)
+        for k in range(k0, len(wb) - 1):
+            a, b = max(wb[k], lo), min(wb[k + 1], hi + 1)
+            if a >= b:
+                break
+            word_text = text[a:b].strip()
             if len(word_text) == 0:
                 continue
-            idx = [r for r in idx if text[r] != " "]
+            idx = [r for r in range(a, b) if text[r] != " "]
             word_start = _nanmin(c_start[r] for r in idx)
             word_end = _nanmax(c_end[r] for r in idx)
-            word_score = round(_nanmean([c_score[r] for r in idx]), 3)
+            word_score = _np_round3(_nanmean([c_score[r] for r in idx]))
             rec = {"word": word_text}
-            if not np.isnan(word_start):
+            if word_start == word_start:
                 rec["start"] = word_start
-            if not np.isnan(word_end):
+            if word_end == word_end:
                 rec["end"] = word_end
-            if not np.isnan(word_score):
+            if word_score == word_score:
                 rec["score"] = word_score
             words.append(rec)
         sub = {"text": sentence_text, "start": sentence_start, "end": sentence_end, "words": words}

@@ -241,10 +241,15 @@ struct AttnArgs {
     const float* q;
     const float* k;
     const float* v;
-    float* o;  // [B, T, H, 64]
+    float* o;  // [B, T, H, 64] (packed: [rows, H, 64])
     int B, H, T;
     int64_t sqb, sqh, sqt, skb, skh, skt, svb, svh, svt;  // element strides (head dim: 1)
     float scale_log2;                                      // softmax scale * log2(e)
+    // packed segments (wx_attention_f32_packed): segment s owns rows [seg_rows[s], seg_rows[s+1])
+    // and work units [seg_units[s], seg_units[s+1]) (H x its 32-query tiles, head-major)
+    const int32_t* seg_rows;
+    const int32_t* seg_units;
+    int nseg;
 };
 
 #ifndef WX_ATTN_SPLIT
@@ -260,29 +265,54 @@ constexpr int kAttnSplit = WX_ATTN_SPLIT;  // waves per 32-query tile, each over
 // keeps everything in 203 VGPRs instead of splitting 194 / 48 with AGPR copies (A/B: 1-2% faster).
 // A third wave per SIMD (168 registers: V loaded behind the S chain instead of a tile ahead,
 // 2 spills) was 10-15% slower.
-__global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu(2))) void attn_f32_kernel(AttnArgs a) {
-    const int T = a.T;
-    const int nq = (T + 31) / 32;
-    int tile, bh;
+// SPLIT waves per 32-query tile (each over every SPLIT-th 32-key tile; SPLIT = 1: one wave, no
+// merge); PACKED: one launch over many segments of their own lengths (rows packed back to back)
+template <int SPLIT, bool PACKED>
+__global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2))) void attn_f32_kernel(AttnArgs a) {
+    int T, tile, h;
+    int64_t row0;  // o row of query 0 of this batch entry / segment
+    const float *Q, *K, *V;
+    // 1-D grid, block L runs on XCD L % 8 (round-robin dispatch): hand each XCD a contiguous
+    // run of (head, query tile) units, so the blocks sharing one head's K / V (768 KB at
+    // T = 1499) meet in one XCD's L2 instead of all eight
+    unsigned w;
     if (WX_ATTN_XCD) {
-        // 1-D grid, block L runs on XCD L % 8 (round-robin dispatch): hand each XCD a contiguous
-        // run of (head, query tile) units, so the blocks sharing one head's K / V (768 KB at
-        // T = 1499) meet in one XCD's L2 instead of all eight
         const unsigned L = blockIdx.x, n = gridDim.x, x = L % 8, i = L / 8, q = n / 8, r = n % 8;
-        const unsigned w = x * q + min(x, r) + i;
-        tile = (int)(w % (unsigned)nq);
-        bh = (int)(w / (unsigned)nq);
+        w = x * q + min(x, r) + i;
     } else {
-        tile = blockIdx.x;
-        bh = blockIdx.y;
+        w = blockIdx.x;
+    }
+    if (PACKED) {
+        // the segment owning unit w: the last s with seg_units[s] <= w (empty segments own no
+        // units, so the last such s is never one of them)
+        int lo = 0, hi = a.nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((unsigned)a.seg_units[mid] <= w) lo = mid;
+            else hi = mid - 1;
+        }
+        row0 = a.seg_rows[lo];
+        T = a.seg_rows[lo + 1] - (int)row0;
+        const int nq = (T + 31) / 32;
+        const int u = (int)w - a.seg_units[lo];
+        tile = u % nq;
+        h = u / nq;
+        Q = a.q + row0 * a.sqt + h * a.sqh;
+        K = a.k + row0 * a.skt + h * a.skh;
+        V = a.v + row0 * a.svt + h * a.svh;
+    } else {
+        T = a.T;
+        const int nq = (T + 31) / 32;
+        tile = (int)(w % (unsigned)nq);
+        const int bh = (int)(w / (unsigned)nq);
+        const int b = bh / a.H;
+        h = bh % a.H;
+        row0 = (int64_t)b * T;
+        Q = a.q + b * a.sqb + h * a.sqh;
+        K = a.k + b * a.skb + h * a.skh;
+        V = a.v + b * a.svb + h * a.svh;
     }
     const int q0 = tile * 32;
-    const int b = bh / a.H;
-    const int h = bh % a.H;
-    const int64_t row0 = (int64_t)b * T;  // o row of query 0 of this batch entry
-    const float* Q = a.q + b * a.sqb + h * a.sqh;
-    const float* K = a.k + b * a.skb + h * a.skh;
-    const float* V = a.v + b * a.svb + h * a.svh;
     const int l = threadIdx.x & 63, r = l & 31, hf = l >> 5, wv = threadIdx.x >> 6;
     float qv[32];
     {
@@ -321,7 +351,7 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
         }
     };
     if (32 * wv < T) load_kv(32 * wv, kv, va, vb);
-    for (int k0 = 32 * wv; k0 < T; k0 += 32 * kAttnSplit) {
+    for (int k0 = 32 * wv; k0 < T; k0 += 32 * SPLIT) {
         f32x16 s;
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[i] = 0.f;
@@ -329,7 +359,7 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
         for (int j = 0; j < 32; ++j) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qv[j], s, 0, 0, 0);
         float van[16], vbn[16];
         {
-            const int kn = min(k0 + 32 * kAttnSplit, T - 1);  // (past the end: a harmless re-read)
+            const int kn = min(k0 + 32 * SPLIT, T - 1);  // (past the end: a harmless re-read)
             load_kv(kn, kv, van, vbn);  // kv is dead once the S chain has been issued
         }
         float mx = -INFINITY;
@@ -372,7 +402,8 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
         }
     }
     // merge the waves' partial softmax states (m, lsum, O^T) in wave 0
-    __shared__ float red[kAttnSplit - 1][34][64];
+    if constexpr (SPLIT > 1) {
+    __shared__ float red[SPLIT - 1][34][64];
     if (wv > 0) {
         float* o = &red[wv - 1][0][l];
         o[0] = m;
@@ -387,7 +418,7 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
     if (wv > 0) return;
     float mt = m;
 #pragma unroll
-    for (int w = 0; w < kAttnSplit - 1; ++w) mt = fmaxf(mt, red[w][0][l]);
+    for (int w = 0; w < SPLIT - 1; ++w) mt = fmaxf(mt, red[w][0][l]);
     {
         const float c = __builtin_amdgcn_exp2f(m - mt);
         lsum *= c;
@@ -398,7 +429,7 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
         }
     }
 #pragma unroll
-    for (int w = 0; w < kAttnSplit - 1; ++w) {
+    for (int w = 0; w < SPLIT - 1; ++w) {
         const float c = __builtin_amdgcn_exp2f(red[w][0][l] - mt);  // a wave without keys: 0
         lsum += red[w][1][l] * c;
 #pragma unroll
@@ -406,6 +437,7 @@ __global__ __launch_bounds__(64 * kAttnSplit) __attribute__((amdgpu_waves_per_eu
             o0[i] += red[w][2 + i][l] * c;
             o1[i] += red[w][18 + i][l] * c;
         }
+    }
     }
     if (q0 + r >= T) return;
     const float inv = 1.0f / lsum;
@@ -565,9 +597,60 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     a.svh = v_strides[1];
     a.svt = v_strides[2];
     a.scale_log2 = scale * 1.4426950408889634f;
-    const dim3 grid = WX_ATTN_XCD ? dim3((unsigned)((int64_t)(T + 31) / 32 * B * H))
-                                  : dim3((unsigned)((T + 31) / 32), (unsigned)(B * H));
-    hipLaunchKernelGGL(attn_f32_kernel, grid, dim3(64 * kAttnSplit), 0, reinterpret_cast<hipStream_t>(stream), a);
+    a.seg_rows = a.seg_units = nullptr;
+    a.nseg = 0;
+    const dim3 grid((unsigned)((int64_t)(T + 31) / 32 * B * H));
+    hipLaunchKernelGGL((attn_f32_kernel<kAttnSplit, false>), grid, dim3(64 * kAttnSplit), 0,
+                       reinterpret_cast<hipStream_t>(stream), a);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_attention_f32_packed(const float* q, const float* k, const float* v, float* o, int32_t nseg,
+                                       const int32_t* seg_rows, const int32_t* seg_units, int32_t n_units,
+                                       int32_t H, int32_t D, const int64_t* q_strides, const int64_t* k_strides,
+                                       const int64_t* v_strides, float scale, int32_t split, void* stream) {
+    using namespace wxe;
+    if (nseg < 0 || H <= 0 || D != 64 || n_units < 0 || !q || !k || !v || !o || !q_strides || !k_strides ||
+        !v_strides)
+        return WX_E_INVALID;
+    if (nseg == 0 || n_units == 0) return WX_OK;
+    if (!seg_rows || !seg_units) return WX_E_INVALID;
+    const int64_t* st[3] = {q_strides, k_strides, v_strides};
+    const float* pt[3] = {q, k, v};
+    for (int i = 0; i < 3; ++i) {  // 16-byte rows (float4 reads of Q / K)
+        if ((reinterpret_cast<uintptr_t>(pt[i]) & 15) || (st[i][0] & 3) || (st[i][1] & 3)) return WX_E_INVALID;
+    }
+    if (reinterpret_cast<uintptr_t>(o) & 15) return WX_E_INVALID;
+    AttnArgs a;
+    a.q = q;
+    a.k = k;
+    a.v = v;
+    a.o = o;
+    a.B = 1;
+    a.H = H;
+    a.T = 0;
+    a.sqb = a.skb = a.svb = 0;
+    a.sqh = q_strides[0];
+    a.sqt = q_strides[1];
+    a.skh = k_strides[0];
+    a.skt = k_strides[1];
+    a.svh = v_strides[0];
+    a.svt = v_strides[1];
+    a.scale_log2 = scale * 1.4426950408889634f;
+    a.seg_rows = seg_rows;
+    a.seg_units = seg_units;
+    a.nseg = nseg;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // a few segments' units leave SIMDs idle unless each query tile's keys are split over waves;
+    // with ~10 units per CU or more, one wave per tile (no merge) keeps them as busy
+    if (split <= 0) split = n_units >= 2560 ? 1 : 4;
+    switch (split) {
+        case 1: hipLaunchKernelGGL((attn_f32_kernel<1, true>), dim3((unsigned)n_units), dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((attn_f32_kernel<2, true>), dim3((unsigned)n_units), dim3(128), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((attn_f32_kernel<4, true>), dim3((unsigned)n_units), dim3(256), 0, s, a); break;
+        default: return WX_E_INVALID;
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

@@ -230,6 +230,8 @@ def _patched_forward(self, x):
 
 
 _ATTN_NAME = "wx_f32"
+_PACK = threading.local()  # .segs: the PackedSegments of the packed encoder running on this thread
+_PACK_SPLIT = int(os.environ.get("WX_ATTN_PACKED_SPLIT", "0"))  # waves per query tile (0: by size)
 
 
 def _wx_attention(module, query, key, value, attention_mask, dropout: float = 0.0, scaling=None, **kwargs):
@@ -245,6 +247,10 @@ def _wx_attention(module, query, key, value, attention_mask, dropout: float = 0.
         from . import _lib
 
         scale = scaling if scaling is not None else query.shape[-1] ** -0.5
+        segs = getattr(_PACK, "segs", None)
+        if segs is not None and query.shape[0] == 1 and query.shape[2] == segs.rows:
+            # the packed encoder (packed_logits): each segment attends only to its own rows
+            return _lib.attention_f32_packed(query, key, value, scale, segs, _PACK_SPLIT), None
         return _lib.attention_f32(query, key, value, scale), None
     return _orig_attention(module)(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
                                    **kwargs)
@@ -509,3 +515,232 @@ def n_frames(n_samples: int, model: Optional[torch.nn.Module] = None) -> int:
 def log_softmax_into(logits: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """torch.log_softmax(logits, -1) written into `out` (a row slice of the CSR matrix)."""
     return torch._log_softmax(logits, -1, False, out=out)
+
+
+# ------------------------------------------------------------------------------------------
+# Packed encoder: many segments in one transformer pass.
+#
+# The reference runs one unpadded forward per segment (alignment.py:217-233); a 30 s segment
+# gives the encoder 1,499 rows, too few to fill 256 CUs: its GEMMs pick 32 x 64 tiles and its
+# attention launches 564 query tiles.  Everything in the encoder except attention, the
+# positional conv and the feature encoder is row-wise (LayerNorm, the q/k/v / out / feed-forward
+# projections, GELU, lm_head), so segments can be stacked along rows with no padding and no
+# interaction: the positional conv runs per segment (its zero padding at each segment's ends),
+# attention through wx_attention_f32_packed (each segment attends to its own rows only), the
+# rest once over all rows.  Per segment this is the reference's computation; only the GEMMs'
+# tiling (their fp32 summation order) differs.  The packed rows are exactly the CSR emission
+# layout the DP reads, so log_softmax writes the whole pack at once.
+
+_PACK_ENCODERS = ("Wav2Vec2Encoder", "Wav2Vec2EncoderStableLayerNorm")
+
+
+def packed_supported(model: torch.nn.Module) -> bool:
+    """Whether packed_logits can run this model: a prepared (prepare_model) transformers
+    Wav2Vec2ForCTC-shaped model in eval mode whose attention is wx_attention_f32, without
+    adapters (WX_NO_PACKED=1: never)."""
+    if os.environ.get("WX_NO_PACKED") or model.training or not getattr(model, "_wx_gemm_conv", False):
+        return False
+    w2v = getattr(model, "wav2vec2", None)
+    head = getattr(model, "lm_head", None)
+    if w2v is None or not isinstance(head, torch.nn.Linear) or getattr(w2v, "adapter", None) is not None:
+        return False
+    enc = getattr(w2v, "encoder", None)
+    cfg = getattr(model, "config", None)
+    if (type(enc).__name__ not in _PACK_ENCODERS or cfg is None or getattr(cfg, "_attn_implementation", None) != _ATTN_NAME
+            or not hasattr(w2v, "feature_extractor") or not hasattr(w2v, "feature_projection")
+            or not hasattr(enc, "pos_conv_embed")):
+        return False
+    return all(getattr(layer, "adapter_layer", None) is None for layer in enc.layers)
+
+
+def _packed_encoder(enc, h: torch.Tensor, segs) -> torch.Tensor:
+    """Wav2Vec2Encoder(.StableLayerNorm).forward (no mask, eval) over packed rows h [1, R, D]."""
+    from . import _lib
+
+    pos = torch.empty_like(h)
+    for a, b in zip(segs.offsets[:-1], segs.offsets[1:]):
+        if b > a:
+            pos[:, a:b] = enc.pos_conv_embed(h[:, a:b])
+    stable = type(enc).__name__ == "Wav2Vec2EncoderStableLayerNorm"
+    ln = enc.layer_norm
+    if stable:
+        h = h + pos
+    elif _addln_ok(enc, h, (ln,)):
+        h = _lib.add_layernorm(h, pos, ln.weight, ln.bias, ln.eps)
+    else:
+        h = ln(h + pos)
+    _PACK.segs = segs
+    try:
+        for layer in enc.layers:
+            h = layer(h, attention_mask=None)[0]
+    finally:
+        _PACK.segs = None
+    return ln(h) if stable else h
+
+
+_FE_KINDS = {"Wav2Vec2GroupNormConvLayer": "group", "Wav2Vec2LayerNormConvLayer": "layer",
+             "Wav2Vec2NoLayerNormConvLayer": "none"}
+
+
+def _fe_layers(fe):
+    """(kind, conv, norm, activation) per feature-encoder layer when every layer is one of
+    transformers' three conv-layer classes with a plain (ungrouped, unpadded, dilation 1) conv;
+    None otherwise."""
+    out = []
+    for layer in getattr(fe, "conv_layers", ()):
+        kind = _FE_KINDS.get(type(layer).__name__)
+        conv = getattr(layer, "conv", None)
+        if (kind is None or not isinstance(conv, torch.nn.Conv1d) or conv.groups != 1 or conv.dilation != (1,)
+                or isinstance(conv.padding, str) or conv.padding != (0,) or conv.padding_mode != "zeros"):
+            return None
+        norm = getattr(layer, "layer_norm", None) if kind != "none" else None
+        if kind == "group" and not (isinstance(norm, torch.nn.GroupNorm) and norm.num_groups == conv.out_channels
+                                    and conv.out_channels % 4 == 0):
+            return None
+        if kind == "layer" and not isinstance(norm, torch.nn.LayerNorm):
+            return None
+        out.append((kind, conv, norm, layer.activation))
+    return out or None
+
+
+def _tm_conv(conv: torch.nn.Conv1d, x: torch.Tensor, Lout: int) -> torch.Tensor:
+    """Time-major conv of a packed buffer: x [L, Cin] (or [L] samples for Cin == 1) ->
+    [Lout, Cout], y[t] = bias + sum_j x[s t + j] W_j (tap GEMMs on strided row views)."""
+    (k,) = conv.kernel_size
+    (s,) = conv.stride
+    b = conv.bias
+    Cout = conv.out_channels
+    if conv.in_channels == 1:
+        x1 = x.reshape(-1)
+        patches = x1.as_strided((Lout, k), (s, 1))
+        w = _tap_weights(conv).reshape(k, Cout)
+        return torch.addmm(b, patches, w) if b is not None else torch.mm(patches, w)
+    wt = _tap_weights(conv)  # [k, Cin, Cout]
+    out = torch.empty((Lout, Cout), dtype=x.dtype, device=x.device)
+    for j in range(k):
+        xj = x[j: j + s * (Lout - 1) + 1: s]
+        if j == 0:
+            if b is not None:
+                torch.addmm(b, xj, wt[0], out=out)
+            else:
+                torch.mm(xj, wt[0], out=out)
+        else:
+            out.addmm_(xj, wt[j])
+    return out
+
+
+def _act_(act, y: torch.Tensor) -> torch.Tensor:
+    if _is_erf_gelu(act):
+        torch._C._nn.gelu_(y)
+        return y
+    return act(y)
+
+
+def packed_features(fe, layers, waveforms, segs, dev) -> torch.Tensor:
+    """The feature encoder of every waveform in one pass per layer: [segs.rows, C] time-major,
+    rows packed like `segs`.
+
+    The waveforms are laid out back to back in one sample buffer, each from an offset that is
+    a multiple of the product P of the layers' strides (320 for wav2vec2), zero-filled between
+    (and up to the reference's 400-sample minimum, alignment.py:217-224).  A layer of stride s
+    maps input row s (o + t) + j to output row o + t, so with every segment's input offset a
+    multiple of s its outputs start at offset / s and read only its own inputs: one GEMM per
+    tap over the whole buffer computes every segment's conv exactly as alone; the few rows
+    between segments (outputs that straddle two of them) are computed and ignored.  The
+    group-norm layer (per-channel statistics over one segment's time) runs per segment on its
+    own rows.  The last layer's segment rows are gathered into the packed layout."""
+    from . import _lib
+
+    ks = [(c.kernel_size[0], c.stride[0]) for _, c, _, _ in layers]
+    P = 1
+    for _, st in ks:
+        P *= st
+    ns = [max(int(w.shape[-1]), 400) for w in waveforms]
+    regions = [-(-n // P) * P for n in ns]
+    offs = [0]
+    for r in regions:
+        offs.append(offs[-1] + r)
+    x = torch.zeros(offs[-1] + P, dtype=torch.float32, device=dev)
+    for w, o in zip(waveforms, offs):
+        w1 = w.reshape(-1)
+        x[o: o + w1.shape[0]].copy_(w1, non_blocking=True)
+    offs = offs[:-1]
+    lens = ns
+    X = x
+    for (kind, conv, norm, act), (k, st) in zip(layers, ks):
+        Lg = X.shape[0]
+        Lout = (Lg - k) // st + 1
+        new_offs = [o // st for o in offs]
+        new_lens = [(n - k) // st + 1 if n >= k else 0 for n in lens]
+        if kind == "group":
+            gelu = _is_erf_gelu(act)
+            if (conv.in_channels == 1 and k <= 16 and not os.environ.get("WX_NO_CONV0_FUSED")):
+                Y = torch.empty((Lout, conv.out_channels), dtype=torch.float32, device=dev)
+                w = _weight(conv)
+                for o, n, oo, lo in zip(offs, lens, new_offs, new_lens):
+                    _lib.conv0_channel_norm(X[o: o + n], w, conv.bias, st, norm.weight, norm.bias, norm.eps, gelu,
+                                            out=Y[oo: oo + lo])
+            else:
+                Y = _tm_conv(conv, X, Lout)
+                for oo, lo in zip(new_offs, new_lens):
+                    _lib.channel_norm(Y[oo: oo + lo], norm.weight, norm.bias, norm.eps, gelu, out=Y[oo: oo + lo])
+            if not gelu:
+                Y = act(Y)
+        else:
+            Y = _tm_conv(conv, X, Lout)
+            if kind == "layer":
+                Y = norm(Y)
+            Y = _act_(act, Y)
+        X, offs, lens = Y, new_offs, new_lens
+    if lens != segs.lengths:
+        raise ValueError(f"feature encoder frame counts {lens} differ from the packed layout's {segs.lengths}")
+    if offs == segs.offsets[:-1]:
+        return X[: segs.rows]
+    idx = torch.cat([torch.arange(o, o + n, dtype=torch.int64) for o, n in zip(offs, lens)])
+    return X.index_select(0, idx.pin_memory().to(dev, non_blocking=True))
+
+
+def packed_logits(model: torch.nn.Module, waveforms, segs, streams) -> torch.Tensor:
+    """The [R, V] logits of every waveform (segments packed by rows as `segs`, a
+    _lib.PackedSegments of their frame counts) on the current stream: feature encoders per
+    segment, round-robin over `streams` (each segment's features joined into the pack by a
+    copy on the current stream), then one packed projection / encoder / lm_head pass.
+    Raises ValueError when a feature encoder's frame count is not segs' (caller falls back)."""
+    from . import _lib
+
+    w2v = model.wav2vec2
+    cur = torch.cuda.current_stream()
+    dev = cur.device
+    C = int(w2v.config.conv_dim[-1])
+    layers = None if os.environ.get("WX_NO_PACKED_FE") else _fe_layers(w2v.feature_extractor)
+    if layers is not None:
+        with torch.inference_mode():
+            feats = packed_features(w2v.feature_extractor, layers, waveforms, segs, dev)
+            h, _ = w2v.feature_projection(feats[None])
+            del feats
+            h = _packed_encoder(w2v.encoder, h, segs)
+            return model.lm_head(h)[0]
+    feats = torch.empty((segs.rows, C), dtype=torch.float32, device=dev)
+    with torch.inference_mode():
+        for st in streams:
+            st.wait_stream(cur)
+        for i, w in enumerate(waveforms):
+            a, b = segs.offsets[i], segs.offsets[i + 1]
+            st = streams[i % len(streams)]
+            with torch.cuda.stream(st):
+                x = w.to(dev, non_blocking=True)
+                if x.dim() == 1:
+                    x = x[None]
+                if x.shape[-1] < 400:  # alignment.py:217-224 (the model's receptive field)
+                    x = F.pad(x, (0, 400 - x.shape[-1]))
+                f = w2v.feature_extractor(x)  # [1, C, T] (a view of a time-major buffer)
+            if tuple(f.shape) != (1, C, b - a):
+                cur.wait_stream(st)
+                raise ValueError(f"feature encoder gave {tuple(f.shape)} for segment {i}, expected (1, {C}, {b - a})")
+            cur.wait_stream(st)
+            feats[a:b].copy_(f[0].transpose(0, 1))
+            f.record_stream(cur)
+        h, _ = w2v.feature_projection(feats[None])
+        del feats
+        h = _packed_encoder(w2v.encoder, h, segs)
+        return model.lm_head(h)[0]

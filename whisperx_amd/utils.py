@@ -12,15 +12,15 @@ def interpolate_nans(x, method="nearest"):
 
     Accepts a pandas Series (returns a Series, like the reference) or a list of floats
     (returns a list; NaN-free input is returned as is without touching pandas)."""
-    import pandas as pd
-
-    if isinstance(x, pd.Series):
+    if type(x).__name__ == "Series":
         if x.notnull().sum() > 1:
             return x.interpolate(method=method).ffill().bfill()
         return x.ffill().bfill()
     vals = [float(v) for v in x]
     if all(v == v for v in vals):
         return vals
+    import pandas as pd  # (only when there is something to interpolate: its import costs ~1 s)
+
     s = pd.Series(vals, dtype="float64")
     if s.notnull().sum() > 1:
         s = s.interpolate(method=method)
