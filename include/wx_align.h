@@ -255,6 +255,18 @@ int wx_attention_f32_packed(const float* q, const float* k, const float* v, floa
                             const int64_t* q_strides, const int64_t* k_strides, const int64_t* v_strides, float scale,
                             int32_t split, void* stream);
 
+/* wav2vec2 positional convolution over packed segments (alignment.py:226-233: the encoder's
+ * Wav2Vec2PositionalConvEmbedding, run per segment): for each segment s (rows [seg_rows[s],
+ * seg_rows[s + 1]) of h [rows, D], 16-byte aligned) out[t] = GELU_erf(bias + conv(h)[t]) (+ h[t]
+ * when residual), conv = Conv1d(D, D, K = 128, padding 64, groups G) with zero padding at the
+ * segment's ends and the last output dropped (transformers' SamePadLayer).  D / G in {48, 64}.
+ * w_packed: [G][K][Cg / 4][Cg][4], w_packed[g][j][i / 4][o][i % 4] = weight[g Cg + o][i][j].
+ * seg_tiles (device, nseg + 1): prefix of ceil(T_s / 128), n_tiles its last entry.  out must not
+ * alias h.  f32 MFMA: equal to torch's conv to fp32 tolerance, not bit-identical. */
+int wx_posconv_packed(const float* h, int32_t D, const float* w_packed, const float* bias, int32_t G, int32_t K,
+                      int32_t nseg, const int32_t* seg_rows, const int32_t* seg_tiles, int32_t n_tiles,
+                      int32_t residual, float* out, void* stream);
+
 /* wav2vec2 encoder layer's residual add + LayerNorm (alignment.py:226-233, the emission
  * forward: `layer_norm(residual + x)` twice per layer): for each of `rows` rows of D floats
  * (D in {256, 512, 768, 1024}; row strides a_stride / b_stride elements, multiples of 4; all

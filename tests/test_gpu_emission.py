@@ -131,6 +131,36 @@ def test_attention_f32_packed_vs_fp64(split):
         torch.testing.assert_close(got[:, a:b], ref, rtol=1e-5, atol=2e-5, msg=f"segment rows [{a}, {b})")
 
 
+@pytest.mark.parametrize("D,residual", [(768, True), (768, False), (1024, True)])
+def test_posconv_packed_vs_torch(D, residual):
+    """wx_posconv_packed (the positional conv embedding of every packed segment in one launch:
+    grouped K = 128 conv with each segment's own zero padding, last output dropped, erf GELU,
+    optionally + h) against transformers' Wav2Vec2PositionalConvEmbedding on each segment
+    alone, fp32 tolerance; ragged lengths around the 128-frame tile and the 64-frame padding."""
+    from transformers import Wav2Vec2Config
+    from transformers.models.wav2vec2.modeling_wav2vec2 import Wav2Vec2PositionalConvEmbedding
+
+    from whisperx_amd import _lib, emission
+
+    torch.manual_seed(D + residual)
+    cfg = Wav2Vec2Config(hidden_size=D, num_attention_heads=D // 64)
+    pce = Wav2Vec2PositionalConvEmbedding(cfg).cuda().eval()
+    pc = emission._posconv_weights(pce)
+    assert pc is not None
+    lengths = [1499, 1, 63, 64, 65, 200, 0, 128, 129, 2999]
+    segs = _lib.PackedSegments(lengths)
+    h = torch.randn(1, segs.rows, D, device="cuda")
+    got = _lib.posconv_packed(h, pc[0], pc[1], pc[2], pc[3], segs, residual=residual)
+    with torch.no_grad():
+        for a, b in zip(segs.offsets[:-1], segs.offsets[1:]):
+            if b == a:
+                continue
+            ref = pce(h[:, a:b])
+            if residual:
+                ref = ref + h[:, a:b]
+            torch.testing.assert_close(got[:, a:b], ref, rtol=1e-4, atol=1e-4, msg=f"segment rows [{a}, {b})")
+
+
 def _packed_vs_per_segment(m, V, lengths, tol=5e-5):
     """emission.packed_logits over ragged waveforms against the stock per-segment forward."""
     from whisperx_amd import _lib, alignment, emission
@@ -163,7 +193,11 @@ def _packed_vs_per_segment(m, V, lengths, tol=5e-5):
         worst = max(worst, err)
         assert err <= tol, f"segment {i} ({lengths[i]} samples): max |packed - stock| = {err}"
         assert torch.equal(g.argmax(-1), r.argmax(-1)), f"segment {i}: frame argmax differs"
-        assert torch.equal(csr[i], g), f"segment {i}: _emissions differs from packed_logits"
+        # (_emissions packs differently — its last pack's quarter runs alone — so its GEMM
+        # tiling, and only that, may differ)
+        err2 = float((csr[i] - r).abs().max())
+        assert err2 <= tol, f"segment {i}: max |_emissions - stock| = {err2}"
+        assert torch.equal(csr[i].argmax(-1), r.argmax(-1)), f"segment {i}: _emissions frame argmax differs"
     return worst
 
 
@@ -266,7 +300,7 @@ def test_emissions_fan_out_fresh_parametrised_model():
     torch.manual_seed(2)
     m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32)).cuda().eval()
     pos = m.wav2vec2.encoder.pos_conv_embed.conv
-    assert getattr(pos, "parametrizations", None) is not None and not hasattr(pos, "_wx_w_cache")
+    assert getattr(pos, "parametrizations", None) is not None and pos not in emission._W_CACHE
     g = torch.Generator().manual_seed(3)
     audio = (torch.randn(1, 80 * 16000, generator=g) * 0.1).cuda()
     wavs = [audio[:, : 60 * 16000]] + [audio[:, 16000 * k: 16000 * k + 16000 + 1234 * k] for k in range(1, 12)]

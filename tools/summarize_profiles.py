@@ -1,4 +1,4 @@
-"""Condense gpurun_out/prof_ROUND/<leg>/ (tools/profile_round2.sh) into profiles/:
+"""Condense gpurun_out/prof_ROUND/<leg>/ (tools/profile_round.sh) into profiles/:
 ROUND_<leg>_kernel_stats.csv (rocprofv3 --stats) and ROUND_profile_summary.json with, per leg,
 the kernel's rocprof average duration, algorithmic bytes per launch, PMC
 traffic per launch (FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 rule + WRITE_SIZE)

@@ -83,6 +83,7 @@ SIGNATURES = {
     "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
+    "wx_posconv_packed": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
     "wx_attention_f32_packed": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
                                                _f32, _i32, _vp]),
     "wx_binarize": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _f32, _f32, _f64, _f64, _f64,
@@ -651,15 +652,18 @@ class PackedSegments:
         self.rows = self.offsets[-1]
         self._dev = {}
 
-    def tables(self, device, H: int):
-        key = (str(device), int(H))
+    def tables(self, device, H: int, rows_per_unit: int = 32):
+        """(seg_rows, seg_units, n_units) on `device`: units of `rows_per_unit` rows, H per
+        segment row-tile (attention: 32-row query tiles x heads; positional conv: 128-row
+        tiles, H = 1)."""
+        key = (str(device), int(H), int(rows_per_unit))
         t = self._dev.get(key)
         if t is None:
             units = [0]
             for n in self.lengths:
-                units.append(units[-1] + H * ((n + 31) // 32))
+                units.append(units[-1] + H * ((n + rows_per_unit - 1) // rows_per_unit))
             if units[-1] > 2 ** 31 - 1 or self.rows > 2 ** 31 - 1:
-                raise WXError("attention_f32_packed: more than 2^31 rows or work units")
+                raise WXError("packed segments: more than 2^31 rows or work units")
             host = torch.tensor(self.offsets + units, dtype=torch.int32).pin_memory()
             dev = host.to(device, non_blocking=True)
             n = len(self.lengths) + 1
@@ -686,6 +690,24 @@ def attention_f32_packed(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scal
                                            _ptr(units_t), n_units, H, D, st[0], st[1], st[2], float(scale), int(split),
                                            _stream(q.device)))
     return o
+
+
+def posconv_packed(h: torch.Tensor, w_packed: torch.Tensor, bias, G: int, K: int, segs: PackedSegments,
+                   residual: bool) -> torch.Tensor:
+    """wx_posconv_packed over h [rows, D] (or [1, rows, D]) contiguous fp32: GELU(conv + bias)
+    per segment (+ h with residual), same shape as h."""
+    lib = load()
+    D = int(h.shape[-1])
+    h2 = h.reshape(-1, D)
+    if h2.shape[0] != segs.rows or not h2.is_contiguous() or h2.dtype != torch.float32:
+        raise WXError(f"posconv_packed: h {tuple(h.shape)} is not the {segs.rows} packed rows (contiguous fp32)")
+    out = torch.empty_like(h)
+    rows_t, tiles_t, n_tiles, _ = segs.tables(h.device, 1, 128)
+    with torch.cuda.device(h.device):
+        _check(lib.wx_posconv_packed(_ptr(h2), D, _ptr(w_packed), _ptr(bias) if bias is not None else None, int(G),
+                                     int(K), len(segs.lengths), _ptr(rows_t), _ptr(tiles_t), n_tiles,
+                                     int(bool(residual)), _ptr(out), _stream(h.device)))
+    return out
 
 
 class _StreamWorkspace(Workspace):

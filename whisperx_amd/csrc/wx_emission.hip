@@ -216,6 +216,101 @@ __global__ __launch_bounds__(256) void conv0_apply_kernel(const float* __restric
     }
 }
 
+// The same two passes for wav2vec2's geometry (K = 10 taps, stride 5), register-resident: a
+// wave covers 32 consecutive rows x 64 channels, and the 165 waveform samples those rows read
+// are loaded once (3 coalesced loads per lane) and broadcast per use with v_readlane (the
+// sample index is uniform over the wave), instead of 10 dependent global loads per row
+// (the generic kernels above: ~90 us per pass for a 30 s segment, latency-bound).  fma
+// accumulation (equal to torch's conv to fp32 tolerance, like the generic path).
+constexpr int kC0R = 32;  // rows per wave
+
+template <int K, int S>
+__device__ __forceinline__ float conv0_row(const float (&sv)[((kC0R - 1) * S + K + 63) / 64], int r, const float (&w)[K],
+                                           float b) {
+    float acc = b;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const int k = r * S + j;
+        acc = fmaf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv[k >> 6]), k & 63)), w[j], acc);
+    }
+    return acc;
+}
+
+template <int K, int S>
+__device__ __forceinline__ void conv0_samples(const float* __restrict__ x, int64_t nsamp, int64_t t0,
+                                              float (&sv)[((kC0R - 1) * S + K + 63) / 64]) {
+    constexpr int NV = ((kC0R - 1) * S + K + 63) / 64;
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int64_t i = t0 * S + 64 * v + l;
+        sv[v] = i < nsamp ? x[i] : 0.f;
+    }
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void conv0_stats_rl_kernel(const float* __restrict__ x, int64_t nsamp, int64_t L,
+                                                             const float* __restrict__ wt,
+                                                             const float* __restrict__ bias, int C,
+                                                             double* __restrict__ part /* [nblk][2][C] */) {
+    const int lc = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lc;
+    const int cc = min(c, C - 1);
+    float w[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = wt[(int64_t)cc * K + j];
+    const float b = bias ? bias[cc] : 0.f;
+    const int64_t t0 = ((int64_t)blockIdx.y * 4 + wv) * kC0R;
+    float sv[((kC0R - 1) * S + K + 63) / 64];
+    conv0_samples<K, S>(x, nsamp, t0, sv);
+    const int64_t nr = L - t0;
+    double sm = 0.0, q = 0.0;
+#pragma unroll
+    for (int r = 0; r < kC0R; ++r) {
+        const double d = (double)conv0_row<K, S>(sv, r, w, b);
+        if (r < nr) {
+            sm += d;
+            q = fma(d, d, q);
+        }
+    }
+    __shared__ double ss[4][64], qq[4][64];
+    ss[wv][lc] = sm;
+    qq[wv][lc] = q;
+    __syncthreads();
+    if (wv == 0 && c < C) {
+        sm = (ss[0][lc] + ss[1][lc]) + (ss[2][lc] + ss[3][lc]);
+        q = (qq[0][lc] + qq[1][lc]) + (qq[2][lc] + qq[3][lc]);
+        part[(int64_t)blockIdx.y * 2 * C + c] = sm;
+        part[(int64_t)blockIdx.y * 2 * C + C + c] = q;
+    }
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void conv0_apply_rl_kernel(const float* __restrict__ x, int64_t nsamp, int64_t L,
+                                                             const float* __restrict__ wt,
+                                                             const float* __restrict__ bias, int C,
+                                                             const float* __restrict__ ab, int gelu,
+                                                             float* __restrict__ y) {
+    const int lc = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lc;
+    const int cc = min(c, C - 1);
+    float w[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) w[j] = wt[(int64_t)cc * K + j];
+    const float b = bias ? bias[cc] : 0.f;
+    const float sa = ab[cc], sb = ab[C + cc];
+    const int64_t t0 = ((int64_t)blockIdx.y * 4 + wv) * kC0R;
+    float sv[((kC0R - 1) * S + K + 63) / 64];
+    conv0_samples<K, S>(x, nsamp, t0, sv);
+    const int64_t nr = L - t0;
+#pragma unroll
+    for (int r = 0; r < kC0R; ++r) {
+        float v = conv0_row<K, S>(sv, r, w, b) * sa + sb;
+        if (gelu) v = gelu_erf0(v);
+        if (r < nr && c < C) y[(t0 + r) * C + c] = v;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // wav2vec2 self-attention, fp32 (alignment.py:226-233: the encoder's 12 / 24 attention layers,
 // one unpadded segment per forward, no mask).  torch's fused attention kernel for fp32
@@ -501,6 +596,129 @@ __global__ __launch_bounds__(256) void add_ln_kernel(const float* __restrict__ a
     }
 }
 
+// ------------------------------------------------------------------------------------
+// wav2vec2 positional convolution over packed segments (alignment.py:226-233: the encoder's
+// Wav2Vec2PositionalConvEmbedding — Conv1d(D, D, K = 128, padding K / 2, groups G), the last
+// output dropped, GELU — run per segment, zero padding at each segment's own ends).  As
+// GEMMs it is G x [T, K Cg] x [K Cg, Cg] per segment with a patch operand (im2col of 128
+// shifted rows) that torch had to gather, 4 x 32-tap blocks: 0.42 ms per 30 s segment at
+// ~34 TFLOP/s.  Here one block per (segment, 128-frame tile, group): the tile's input window
+// (255 rows x Cg channels) sits in LDS once and every tap reads its A fragments from it
+// shifted by one row; the group's weights stream tap by tap through a double-buffered LDS
+// slab (register-staged a tap ahead).  4 waves x 32 frames x Cg outputs on
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chains: not bit-identical to torch's conv, whose
+// summation order differs); bias, erf GELU and optionally the residual (h + pos) fused.
+constexpr int kPcFrames = 128;  // output frames per block (4 waves x 32)
+constexpr int kPcK = 128;       // taps (wav2vec2's num_conv_pos_embeddings)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct PosConvArgs {
+    const float* h;      // [rows, D] packed segments
+    const float* w;      // [G][K][Cg / 4][Cg][4]: w[g][j][i / 4][o][i % 4] = conv.weight[g Cg + o][i][j]
+    const float* bias;   // [D] or null
+    float* out;          // [rows, D]
+    const int32_t* seg_rows;
+    const int32_t* seg_tiles;  // prefix of ceil(T_s / kPcFrames)
+    int nseg, D;
+    int residual;
+};
+
+template <int CG>
+__global__ __launch_bounds__(256) void posconv_kernel(PosConvArgs a) {
+    constexpr int RS = CG + 4;  // window row stride (floats): 16-B rows, banks spread over 16 rows
+    constexpr int WR = kPcFrames + kPcK - 1;
+    constexpr int NOB = CG / 16, NIC = CG / 16;
+    constexpr int NB4 = CG * CG / 4;  // float4 per tap of the group's weights
+    constexpr int PER = (NB4 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float xa[WR * RS];
+    __shared__ __attribute__((aligned(16))) float wb[2][CG * CG];
+    const int g = blockIdx.y;
+    const int w = blockIdx.x;
+    int lo = 0, hi = a.nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.seg_tiles[mid] <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    const int row0 = a.seg_rows[lo];
+    const int T = a.seg_rows[lo + 1] - row0;
+    const int t0 = (w - a.seg_tiles[lo]) * kPcFrames;
+    const float* hg = a.h + (int64_t)row0 * a.D + g * CG;
+    // the input window: row r <-> segment frame t0 - K / 2 + r (zero outside [0, T))
+    for (int e = threadIdx.x; e < WR * (CG / 4); e += 256) {
+        const int r = e / (CG / 4), c4 = e - r * (CG / 4);
+        const int t = t0 - kPcK / 2 + r;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t >= 0 && t < T) v = *reinterpret_cast<const float4*>(hg + (int64_t)t * a.D + 4 * c4);
+        *reinterpret_cast<float4*>(xa + r * RS + 4 * c4) = v;
+    }
+    const float4* wg = reinterpret_cast<const float4*>(a.w) + (int64_t)g * kPcK * NB4;
+    float4 breg[PER];  // (the last slot of a partial tap re-reads a valid element; not stored)
+#define WX_PC_BLOAD(j)                                                                    \
+    _Pragma("unroll") for (int p = 0; p < PER; ++p) breg[p] =                             \
+        wg[(int64_t)(j) * NB4 + min((int)threadIdx.x + 256 * p, NB4 - 1)];
+#define WX_PC_BSTORE(buf)                                                                 \
+    _Pragma("unroll") for (int p = 0; p < PER; ++p) if ((int)threadIdx.x + 256 * p < NB4) \
+        reinterpret_cast<float4*>(wb[buf])[threadIdx.x + 256 * p] = breg[p];
+    WX_PC_BLOAD(0)
+    WX_PC_BSTORE(0)
+    __syncthreads();
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
+    f32x4 acc[2][NOB];
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[fb][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // A fragment rows: frame wv 32 + 16 fb + r16 of the tile, shifted by the tap
+    const float* xrow = xa + (wv * 32 + r16) * RS + 4 * q;
+    for (int j = 0; j < kPcK; ++j) {
+        if (j + 1 < kPcK) {
+            WX_PC_BLOAD(j + 1)
+        }
+        const float* bb = wb[j & 1] + (q * CG + r16) * 4;
+#pragma unroll
+        for (int ic = 0; ic < NIC; ++ic) {
+            float4 av[2], bv[NOB];
+#pragma unroll
+            for (int fb = 0; fb < 2; ++fb) av[fb] = *reinterpret_cast<const float4*>(xrow + (16 * fb + j) * RS + 16 * ic);
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) bv[ob] = *reinterpret_cast<const float4*>(bb + (ic * 4 * CG + 16 * ob) * 4);
+#pragma unroll
+            for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+                for (int ob = 0; ob < NOB; ++ob) {
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].x, bv[ob].x, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].y, bv[ob].y, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].z, bv[ob].z, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].w, bv[ob].w, acc[fb][ob], 0, 0, 0);
+                }
+        }
+        if (j + 1 < kPcK) {
+            WX_PC_BSTORE((j + 1) & 1)
+        }
+        __syncthreads();
+    }
+#undef WX_PC_BLOAD
+#undef WX_PC_BSTORE
+    // accumulator (fb, ob) register v: frame 16 fb + 4 q + v of the wave's 32, output 16 ob + r16
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int t = t0 + wv * 32 + 16 * fb + 4 * q + v;
+            if (t >= T) continue;
+            const int64_t rb = (int64_t)(row0 + t) * a.D + g * CG;
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) {
+                const int c = 16 * ob + r16;
+                float y = acc[fb][ob][v] + (a.bias ? a.bias[g * CG + c] : 0.f);
+                y = gelu_erf0(y);
+                if (a.residual) y += a.h[rb + c];
+                a.out[rb + c] = y;
+            }
+        }
+}
+
 }  // namespace wxe
 
 extern "C" size_t wx_channel_norm_workspace_bytes(int32_t C) {
@@ -541,9 +759,22 @@ extern "C" int wx_conv0_channel_norm(const float* x, int64_t S, int32_t K, int32
     const int64_t L = S >= K ? (S - K) / stride + 1 : 0;
     if (L == 0) return WX_OK;
     if (!workspace || workspace_bytes < wx_conv0_channel_norm_workspace_bytes(L, C)) return WX_E_WORKSPACE;
-    const int64_t nblk = (L + kRows * kC0Rows - 1) / (kRows * kC0Rows);
+    const bool rl = K == 10 && stride == 5;  // wav2vec2's geometry: the register-resident kernels
+    const int64_t rows_per_blk = rl ? 4 * kC0R : kRows * kC0Rows;
+    const int64_t nblk = (L + rows_per_blk - 1) / rows_per_blk;
     if (nblk > 65535) return WX_E_INVALID;  // (grid y; ~4.2 h of 16 kHz audio at stride 5)
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (rl) {
+        double* part = reinterpret_cast<double*>(workspace);
+        float* ab = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
+        const dim3 grid((C + 63) / 64, (unsigned)nblk);
+        hipLaunchKernelGGL((conv0_stats_rl_kernel<10, 5>), grid, dim3(256), 0, st, x, S, L, w, bias, C, part);
+        hipLaunchKernelGGL(conv0_finish_kernel, dim3((C + kCols - 1) / kCols), dim3(kCols * kRows), 0, st, part,
+                           (int)nblk, L, C, gamma, beta, eps, ab);
+        hipLaunchKernelGGL((conv0_apply_rl_kernel<10, 5>), grid, dim3(256), 0, st, x, S, L, w, bias, C, ab, gelu, y);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? WX_OK : (int)e;
+    }
     double* part = reinterpret_cast<double*>(workspace);
     float* ab = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
     const dim3 grid((C + kCols - 1) / kCols, (unsigned)nblk), blk(kCols * kRows);
@@ -673,6 +904,36 @@ extern "C" int wx_add_layernorm(const float* a, const float* b, int64_t rows, in
         case 512: hipLaunchKernelGGL(add_ln_kernel<2>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
         case 768: hipLaunchKernelGGL(add_ln_kernel<3>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
         default: hipLaunchKernelGGL(add_ln_kernel<4>, grid, dim3(256), 0, st, a, b, gamma, beta, eps, rows, a_stride, b_stride, (int64_t)D, y, sum_out); break;
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_posconv_packed(const float* h, int32_t D, const float* w_packed, const float* bias, int32_t G,
+                                 int32_t K, int32_t nseg, const int32_t* seg_rows, const int32_t* seg_tiles,
+                                 int32_t n_tiles, int32_t residual, float* out, void* stream) {
+    using namespace wxe;
+    if (!h || !w_packed || !out || G <= 0 || D <= 0 || D % G || nseg < 0 || n_tiles < 0) return WX_E_INVALID;
+    if (K != kPcK) return WX_E_INVALID;
+    if (nseg == 0 || n_tiles == 0) return WX_OK;
+    if (!seg_rows || !seg_tiles || G > 65535) return WX_E_INVALID;
+    if ((reinterpret_cast<uintptr_t>(h) & 15) || (D & 3)) return WX_E_INVALID;
+    PosConvArgs a;
+    a.h = h;
+    a.w = w_packed;
+    a.bias = bias;
+    a.out = out;
+    a.seg_rows = seg_rows;
+    a.seg_tiles = seg_tiles;
+    a.nseg = nseg;
+    a.D = D;
+    a.residual = residual;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)n_tiles, (unsigned)G);
+    switch (D / G) {
+        case 48: hipLaunchKernelGGL(posconv_kernel<48>, grid, dim3(256), 0, s, a); break;
+        case 64: hipLaunchKernelGGL(posconv_kernel<64>, grid, dim3(256), 0, s, a); break;
+        default: return WX_E_INVALID;
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;

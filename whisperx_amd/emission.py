@@ -32,7 +32,7 @@ PyTorch-ROCm model call, one per segment, but:
   csrc/wx_emission.hip) via transformers' attention interface; torch's fused fp32 attention
   was a third of config 3's GPU time.
 * **One q/k/v GEMM.**  Each self-attention's three projections run as one GEMM on the
-  concatenated weights (cached per call); k_proj / v_proj return column slices of its output,
+  concatenated weights (cached, _QKV_CACHE); k_proj / v_proj return column slices of its output,
   which wx_attention_f32 reads in place (strided views).
 * **No concatenation copy.**  ``log_softmax`` writes each segment's ``[T, V]`` rows straight
   into its slice of the CSR emission matrix the DP kernel reads (``emissions_csr``).
@@ -43,12 +43,23 @@ import contextlib
 import os
 import threading
 import types
+import weakref
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 
 _TAP_BLOCK = 32  # grouped/Cin==1 convs: taps per patch block
+
+
+# Derived weights (the weight_norm'd positional conv's weight, per-tap GEMM operands, the fused
+# q/k/v matrix), per module, outside the module (the caller's model keeps no attributes of
+# ours) and kept across align() calls (rebuilding them took ~0.8 ms of GPU time per call);
+# each entry is keyed on its parameters' (data_ptr, version), so an update rebuilds it, and
+# dies with its module.
+_W_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_TAP_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_QKV_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 def _weight(conv: torch.nn.Conv1d) -> torch.Tensor:
@@ -63,11 +74,11 @@ def _weight(conv: torch.nn.Conv1d) -> torch.Tensor:
     if par is None or "weight" not in par:
         return conv.weight
     key = tuple((p.data_ptr(), p._version) for p in par["weight"].parameters())
-    cached = getattr(conv, "_wx_w_cache", None)
+    cached = _W_CACHE.get(conv)
     if cached is not None and cached[0] == key:
         return cached[1]
     w = conv.weight.detach()
-    conv._wx_w_cache = (key, w)
+    _W_CACHE[conv] = (key, w)
     return w
 
 
@@ -87,7 +98,7 @@ def _tap_weights(conv: torch.nn.Conv1d) -> torch.Tensor:
     # keyed on the module's parameters (a weight_norm'd conv's `weight` is recomputed from
     # weight_g / weight_v by a hook — a new, possibly inference, tensor at every call)
     key = tuple((t.data_ptr(), _version(t)) for t in conv.parameters())
-    cached = getattr(conv, "_wx_tap_cache", None)
+    cached = _TAP_CACHE.get(conv)
     if cached is not None and cached[0] == key:
         return cached[1]
     w = _weight(conv)
@@ -98,7 +109,7 @@ def _tap_weights(conv: torch.nn.Conv1d) -> torch.Tensor:
             t = w.detach().permute(2, 1, 0).contiguous()
         else:
             t = w.detach().reshape(G, Cout // G, Cg, k).permute(0, 3, 2, 1).contiguous()
-    conv._wx_tap_cache = (key, t)
+    _TAP_CACHE[conv] = (key, t)
     return t
 
 
@@ -303,13 +314,13 @@ def _qkv_weights(q: torch.nn.Linear):
     k, v = st["k"], st["v"]
     params = [m.weight for m in (q, k, v)] + [m.bias for m in (q, k, v) if m.bias is not None]
     key = tuple((p.data_ptr(), p._version) for p in params)
-    c = st.get("cache")
+    c = _QKV_CACHE.get(q)
     if c is None or c[0] != key:
         with torch.no_grad():
             w = torch.cat([q.weight, k.weight, v.weight], 0).detach().contiguous()
             b = torch.cat([q.bias, k.bias, v.bias]).detach() if all(m.bias is not None for m in (q, k, v)) else None
         c = (key, w, b)
-        st["cache"] = c
+        _QKV_CACHE[q] = c
     return c[1], c[2]
 
 
@@ -446,8 +457,8 @@ def prepare_model(model: torch.nn.Module) -> torch.nn.Module:
 
 
 def restore_model(model: torch.nn.Module) -> torch.nn.Module:
-    """Undo prepare_model: the original forwards, attention implementation and no cached
-    weights (the model is then exactly what the caller passed in)."""
+    """Undo prepare_model: the original forwards and attention implementation (the model is
+    then exactly what the caller passed in; derived weights stay cached outside it, _W_CACHE)."""
     for mod in model.modules():
         if hasattr(mod, "_wx_orig_forward"):
             orig = mod._wx_orig_forward
@@ -456,10 +467,6 @@ def restore_model(model: torch.nn.Module) -> torch.nn.Module:
             else:
                 mod.forward = orig  # the module had its own instance-level forward
             del mod._wx_orig_forward
-        if hasattr(mod, "_wx_w_cache"):
-            del mod._wx_w_cache
-        if hasattr(mod, "_wx_tap_cache"):
-            del mod._wx_tap_cache
         mod.__dict__.pop("_wx_qkv", None)
     if "_wx_gemm_conv" in model.__dict__:
         del model._wx_gemm_conv
@@ -553,22 +560,60 @@ def packed_supported(model: torch.nn.Module) -> bool:
     return all(getattr(layer, "adapter_layer", None) is None for layer in enc.layers)
 
 
+_PC_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _posconv_weights(pce):
+    """(w_packed, bias, G, K) for wx_posconv_packed when the positional conv embedding is
+    wav2vec2's (Conv1d K = 128, padding 64, G groups of 48 or 64 channels, the last output
+    dropped, erf GELU), else None.  w_packed [G][K][Cg / 4][Cg][4] is cached per module until
+    a parameter changes."""
+    conv = getattr(pce, "conv", None)
+    pad = getattr(pce, "padding", None)
+    if (os.environ.get("WX_NO_POSCONV") or not isinstance(conv, torch.nn.Conv1d)
+            or conv.kernel_size != (128,) or conv.stride != (1,) or conv.dilation != (1,)
+            or isinstance(conv.padding, str) or conv.padding != (64,) or conv.padding_mode != "zeros"
+            or getattr(pad, "num_pad_remove", None) != 1 or not _is_erf_gelu(getattr(pce, "activation", None))):
+        return None
+    G = conv.groups
+    D = conv.out_channels
+    if conv.in_channels != D or D % G or D // G not in (48, 64):
+        return None
+    w = _weight(conv)
+    key = (w.data_ptr(), _version(w)) + tuple((t.data_ptr(), _version(t)) for t in conv.parameters())
+    c = _PC_CACHE.get(conv)
+    if c is None or c[0] != key:
+        Cg = D // G
+        with torch.no_grad():
+            wp = (w.detach().reshape(G, Cg, Cg, 128).permute(0, 3, 2, 1)   # [G, K, Cg_in, Cg_out]
+                  .reshape(G, 128, Cg // 4, 4, Cg).permute(0, 1, 2, 4, 3).contiguous())
+        c = (key, wp)
+        _PC_CACHE[conv] = c
+    return c[1], conv.bias, G, 128
+
+
 def _packed_encoder(enc, h: torch.Tensor, segs) -> torch.Tensor:
     """Wav2Vec2Encoder(.StableLayerNorm).forward (no mask, eval) over packed rows h [1, R, D]."""
     from . import _lib
 
-    pos = torch.empty_like(h)
-    for a, b in zip(segs.offsets[:-1], segs.offsets[1:]):
-        if b > a:
-            pos[:, a:b] = enc.pos_conv_embed(h[:, a:b])
     stable = type(enc).__name__ == "Wav2Vec2EncoderStableLayerNorm"
     ln = enc.layer_norm
-    if stable:
-        h = h + pos
-    elif _addln_ok(enc, h, (ln,)):
-        h = _lib.add_layernorm(h, pos, ln.weight, ln.bias, ln.eps)
+    pc = _posconv_weights(enc.pos_conv_embed) if h.is_contiguous() and h.data_ptr() % 16 == 0 else None
+    if pc is not None:
+        # h + GELU(positional conv) per segment in one kernel (wx_posconv_packed)
+        s = _lib.posconv_packed(h, pc[0], pc[1], pc[2], pc[3], segs, residual=True)
+        h = s if stable else ln(s)
     else:
-        h = ln(h + pos)
+        pos = torch.empty_like(h)
+        for a, b in zip(segs.offsets[:-1], segs.offsets[1:]):
+            if b > a:
+                pos[:, a:b] = enc.pos_conv_embed(h[:, a:b])
+        if stable:
+            h = h + pos
+        elif _addln_ok(enc, h, (ln,)):
+            h = _lib.add_layernorm(h, pos, ln.weight, ln.bias, ln.eps)
+        else:
+            h = ln(h + pos)
     _PACK.segs = segs
     try:
         for layer in enc.layers:
