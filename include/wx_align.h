@@ -303,6 +303,14 @@ int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t
  * where chunk c's first frame lands (non-decreasing).  out[f] = (sum over covering chunks, in
  * chunk order, of max_k scores[c, f - start_frame[c], k]) / (number of them), NaN outputs
  * masked out; `missing` where no chunk covers f.  Feeds wx_binarize on the device. */
+/* VAD producer (vad.py:198-240 -> pyannote PyanNet's LSTM): one bidirectional LSTM layer,
+ * hidden size H = 128, over B sequences of T steps, both directions in one persistent launch.
+ * xp [B][T][2][4H]: each step's input projection x W_ih^T + b_ih + b_hh per direction (gate
+ * order i, f, g, o as torch.nn.LSTM); whh [2][4H][H]: weight_hh of the forward and reverse
+ * direction; y [B][T][2H] (16-byte aligned): h of the forward direction, then the reverse.
+ * h0 = c0 = 0.  fp32; equal to torch.nn.LSTM to fp32 tolerance (f32 MFMA fma chains). */
+int wx_lstm_bidir_layer(const float* xp, const float* whh, float* y, int64_t B, int64_t T, int32_t H, void* stream);
+
 int wx_vad_aggregate(const float* scores, const int64_t* start_frame, int32_t n_chunks,
                      int32_t frames_per_chunk, int32_t n_classes, int64_t n_frames, float missing,
                      float* out, void* stream);

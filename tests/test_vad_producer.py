@@ -199,3 +199,48 @@ def test_sincnet_fused_epilogue_matches_torch_ops(monkeypatch):
     thr = float(0.5 * (vals[i] + vals[i + 1]))
     if vals[i + 1] - vals[i] > 4 * diff:  # (every frame on the same side of thr in both)
         assert merge_chunks(feat_f, 30, onset=thr, offset=thr) == merge_chunks(feat_p, 30, onset=thr, offset=thr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,layers", [(37, 293, 2), (16, 1, 1), (3, 50, 2), (130, 293, 1)])
+def test_lstm_kernel_vs_torch_lstm(B, T, layers):
+    """wx_lstm_bidir_layer (PyanNet's bidirectional LSTM, one persistent launch per layer)
+    through vad_model.lstm_forward against torch.nn.LSTM (fp32): batches that are not a
+    multiple of the kernel's 16 sequences, a single step, both layer counts."""
+    from whisperx_amd import vad_model
+
+    torch.manual_seed(B * 1000 + T)
+    lstm = torch.nn.LSTM(60, 128, num_layers=layers, bidirectional=True, batch_first=True).cuda().eval()
+    x = torch.randn(B, T, 60, device="cuda")
+    with torch.inference_mode():
+        ref = lstm(x)[0]
+        got = vad_model.lstm_forward(lstm, x)
+    assert got.shape == ref.shape == (B, T, 256)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.gpu
+def test_lstm_kernel_producer_scores_and_chunks(monkeypatch):
+    """The VAD producer with the LSTM kernel against torch's LSTM (WX_NO_LSTM_KERNEL=1): window
+    scores within float noise and identical merge_chunks (threshold in the widest score gap)."""
+    from whisperx_amd.vad import merge_chunks
+    from whisperx_amd.vad_model import VoiceActivitySegmentation
+
+    torch.manual_seed(3)
+    vad = VoiceActivitySegmentation(device="cuda:0", batch_size=64)
+    wav = torch.randn(1, 75 * 16000 + 123) * 0.1
+    monkeypatch.delenv("WX_NO_LSTM_KERNEL", raising=False)
+    kern = vad.chunk_scores(wav)
+    feat_k = vad({"waveform": wav, "sample_rate": 16000})
+    monkeypatch.setenv("WX_NO_LSTM_KERNEL", "1")
+    plain = vad.chunk_scores(wav)
+    feat_p = vad({"waveform": wav, "sample_rate": 16000})
+    diff = (kern - plain).abs().max().item()
+    assert diff <= 1e-4
+    vals = np.sort(feat_p.data[:, 0].cpu().numpy())
+    vals = vals[np.isfinite(vals)]
+    lo, hi = len(vals) // 20, 19 * len(vals) // 20
+    i = lo + int(np.argmax(np.diff(vals[lo:hi + 1])))
+    thr = float(0.5 * (vals[i] + vals[i + 1]))
+    assert vals[i + 1] - vals[i] > 4 * diff
+    assert merge_chunks(feat_k, 30, onset=thr, offset=thr) == merge_chunks(feat_p, 30, onset=thr, offset=thr)

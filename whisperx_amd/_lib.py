@@ -83,6 +83,7 @@ SIGNATURES = {
     "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
+    "wx_lstm_bidir_layer": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "wx_posconv_packed": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
     "wx_attention_f32_packed": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
                                                _f32, _i32, _vp]),
@@ -561,6 +562,21 @@ def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slo
     with torch.cuda.device(x_tm.device):
         _check(lib.wx_sincnet_stage_ex(_ptr(x_tm), B, L, C, int(x_tm.stride(0)), int(bool(do_abs)), _ptr(sc), _ptr(sh),
                                        _ptr(g), _ptr(bt), float(eps), float(slope), _ptr(y), _stream(x_tm.device)))
+    return y
+
+
+def lstm_bidir_layer(xp: torch.Tensor, whh: torch.Tensor, B: int, T: int) -> torch.Tensor:
+    """wx_lstm_bidir_layer: one bidirectional LSTM layer (H = 128) over B sequences of T steps
+    from the input projections xp [B, T, 2, 4H] (x W_ih^T + b_ih + b_hh per direction) and
+    whh [2, 4H, H]; returns the outputs [B, T, 2H] (forward then reverse direction)."""
+    lib = load()
+    H = int(whh.shape[-1])
+    if tuple(xp.shape) != (B, T, 2, 4 * H) or tuple(whh.shape) != (2, 4 * H, H) or not xp.is_contiguous() \
+            or not whh.is_contiguous() or xp.dtype != torch.float32 or whh.dtype != torch.float32:
+        raise WXError(f"lstm_bidir_layer: xp {tuple(xp.shape)} / whh {tuple(whh.shape)} are not [B, T, 2, 4H] / [2, 4H, H] fp32")
+    y = torch.empty((B, T, 2 * H), dtype=torch.float32, device=xp.device)
+    with torch.cuda.device(xp.device):
+        _check(lib.wx_lstm_bidir_layer(_ptr(xp), _ptr(whh), _ptr(y), int(B), int(T), H, _stream(xp.device)))
     return y
 
 

@@ -120,6 +120,101 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// PyanNet's bidirectional LSTM layer (pyannote segmentation, called by vad.py:198-240), one
+// persistent kernel per layer for both directions.  MIOpen ran it as 293 time steps x 2
+// directions of a [B, 128] x [128, 512] GEMM launch plus a gate-update launch (~37 k launches
+// per hour of audio, ~29% of the producer's GPU time).  Here the input projection of every
+// step (x W_ih^T + b_ih + b_hh, both directions) is one GEMM before the call (xp), and one
+// workgroup carries 16 sequences of one direction through all T steps: per step
+//   gates[16, 512] = xp[t] + h_{t-1} W_hh^T     (v_mfma_f32_16x16x4_f32: wave w computes gate
+//                                               w's 128 columns, W_hh's fragments held in
+//                                               registers for the whole sequence)
+//   i, f, o = sigmoid, g = tanh -> LDS;  c = f c + i g;  h = o tanh(c) -> LDS (next step's A
+//   operand) and y[b, t, d H + u].
+// fp32 throughout (fma chains in the MFMA, not bit-identical to MIOpen's; tests compare with
+// torch.nn.LSTM at fp32 tolerance).  H = 128 (PyanNet).
+constexpr int kLH = 128;  // hidden size
+constexpr int kLR = 16;   // sequences per workgroup
+
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void lstm_layer_kernel(
+    const float* __restrict__ xp /* [B][T][2][4H] */, const float* __restrict__ whh /* [2][4H][H] */,
+    float* __restrict__ y /* [B][T][2H] */, int B, int T) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    constexpr int RS = kLH + 4;  // h row stride in LDS (floats)
+    __shared__ __attribute__((aligned(16))) float hs[kLR * RS];
+    __shared__ __attribute__((aligned(16))) float gs[4][kLR][kLH];
+    const int d = blockIdx.y;
+    const int b0 = blockIdx.x * kLR;
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
+    // this wave's W_hh fragments, kept for the whole sequence: gate w's rows n = 128 w + 16 tile + r16,
+    // k = 16 kk + 4 q .. + 3
+    const float* wd = whh + (int64_t)d * 4 * kLH * kLH;
+    float4 wf[8][8];  // [tile][kk]
+#pragma unroll
+    for (int tile = 0; tile < 8; ++tile)
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+            wf[tile][kk] = *reinterpret_cast<const float4*>(wd + (int64_t)(128 * w + 16 * tile + r16) * kLH + 16 * kk + 4 * q);
+    for (int i = threadIdx.x; i < kLR * RS; i += 256) hs[i] = 0.f;
+    // cell state: thread owns row e / H, units (e % H) .. +7 for e = 8 threadIdx
+    const int er = (threadIdx.x * 8) / kLH, eu = (threadIdx.x * 8) % kLH;
+    float c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] = 0.f;
+    __syncthreads();
+    for (int s = 0; s < T; ++s) {
+        const int t = d ? T - 1 - s : s;
+        f32x4 acc[8];
+        // xp rows of this step: accumulator (tile, v) <-> row 4 q + v, column 16 tile + r16 of gate w
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int b = min(b0 + 4 * q + v, B - 1);
+            const float* xr = xp + (((int64_t)b * T + t) * 2 + d) * 4 * kLH + 128 * w + r16;
+#pragma unroll
+            for (int tile = 0; tile < 8; ++tile) acc[tile][v] = xr[16 * tile];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const float4 a = *reinterpret_cast<const float4*>(hs + r16 * RS + 16 * kk + 4 * q);
+#pragma unroll
+            for (int tile = 0; tile < 8; ++tile) {
+                acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wf[tile][kk].x, acc[tile], 0, 0, 0);
+                acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wf[tile][kk].y, acc[tile], 0, 0, 0);
+                acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wf[tile][kk].z, acc[tile], 0, 0, 0);
+                acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wf[tile][kk].w, acc[tile], 0, 0, 0);
+            }
+        }
+        // gate activations (PyTorch order i, f, g, o: wave 2 is the tanh gate)
+#pragma unroll
+        for (int tile = 0; tile < 8; ++tile)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float x = acc[tile][v];
+                gs[w][4 * q + v][16 * tile + r16] = w == 2 ? tanhf(x) : sigmoid_f(x);
+            }
+        __syncthreads();
+        float hv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int u = eu + i;
+            const float ig = gs[0][er][u], fg = gs[1][er][u], gg = gs[2][er][u], og = gs[3][er][u];
+            c[i] = fg * c[i] + ig * gg;
+            hv[i] = og * tanhf(c[i]);
+        }
+        *reinterpret_cast<float4*>(hs + er * RS + eu) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+        *reinterpret_cast<float4*>(hs + er * RS + eu + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+        if (b0 + er < B) {
+            float* yr = y + ((int64_t)(b0 + er) * T + t) * 2 * kLH + d * kLH + eu;
+            *reinterpret_cast<float4*>(yr) = make_float4(hv[0], hv[1], hv[2], hv[3]);
+            *reinterpret_cast<float4*>(yr + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace wxv
 
 extern "C" int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t x_window_stride,
@@ -159,4 +254,18 @@ extern "C" int wx_sincnet_stage(const float* x, int64_t B, int64_t L, int32_t C,
     if (x_window_stride < L * (int64_t)C) return WX_E_INVALID;
     return wx_sincnet_stage_ex(x, B, L, C, x_window_stride, do_abs, nullptr, nullptr, gamma, beta, eps, slope, y,
                                stream);
+}
+
+extern "C" int wx_lstm_bidir_layer(const float* xp, const float* whh, float* y, int64_t B, int64_t T, int32_t H,
+                                   void* stream) {
+    using namespace wxv;
+    if (B < 0 || T < 0 || H != kLH || !xp || !whh || !y) return WX_E_INVALID;
+    if (B == 0 || T == 0) return WX_OK;
+    if ((reinterpret_cast<uintptr_t>(whh) & 15) || (reinterpret_cast<uintptr_t>(y) & 15)) return WX_E_INVALID;
+    if ((B + kLR - 1) / kLR > 65535 * 1024L) return WX_E_INVALID;
+    const dim3 grid((unsigned)((B + kLR - 1) / kLR), 2);
+    hipLaunchKernelGGL(lstm_layer_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xp, whh, y,
+                       (int)B, (int)T);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
 }

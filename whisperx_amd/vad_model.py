@@ -36,6 +36,7 @@ import math
 import os
 import pickle
 import types
+import weakref
 from typing import Optional
 
 import numpy as np
@@ -283,6 +284,47 @@ def _fused_epilogue(pool, norm, x) -> bool:
     return C % 4 == 0 and C <= 128 and xt.stride(2) == 1 and xt.stride(1) == C
 
 
+_LSTM_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _lstm_weights(lstm: torch.nn.LSTM, layer: int):
+    """(W_ih of both directions [8H, in], b_ih + b_hh [8H], weight_hh [2, 4H, H]) of one layer,
+    cached per module until a parameter changes."""
+    key = (layer,) + tuple((p.data_ptr(), p._version) for p in lstm.parameters())
+    c = _LSTM_CACHE.get(lstm)
+    if c is None or c[0][1:] != key[1:]:
+        c = (key, {})
+        _LSTM_CACHE[lstm] = c
+    if layer not in c[1]:
+        sfx = [f"_l{layer}", f"_l{layer}_reverse"]
+        with torch.no_grad():
+            wih = torch.cat([getattr(lstm, "weight_ih" + s) for s in sfx], 0).detach().contiguous()
+            b = torch.cat([(getattr(lstm, "bias_ih" + s) + getattr(lstm, "bias_hh" + s)) for s in sfx]).detach()
+            whh = torch.stack([getattr(lstm, "weight_hh" + s) for s in sfx], 0).detach().contiguous()
+        c[1][layer] = (wih, b, whh)
+    return c[1][layer]
+
+
+def lstm_forward(lstm: torch.nn.LSTM, x: torch.Tensor) -> torch.Tensor:
+    """lstm(x)[0] for a batch-first input [B, T, in]: PyanNet's bidirectional LSTM (H = 128,
+    biases, no projection) of an inference forward on a HIP device runs layer by layer as one
+    input-projection GEMM (both directions) + wx_lstm_bidir_layer (the recurrence of both
+    directions in one persistent kernel) instead of MIOpen's per-step launches
+    (WX_NO_LSTM_KERNEL=1: torch's LSTM)."""
+    if (os.environ.get("WX_NO_LSTM_KERNEL") or not x.is_cuda or torch.is_grad_enabled() or lstm.training
+            or not lstm.bidirectional or not lstm.batch_first or lstm.hidden_size != 128 or not lstm.bias
+            or getattr(lstm, "proj_size", 0) or x.dtype != torch.float32 or x.dim() != 3):
+        return lstm(x)[0]
+    from . import _lib
+
+    B, T, _ = x.shape
+    for layer in range(lstm.num_layers):
+        wih, b, whh = _lstm_weights(lstm, layer)
+        xp = torch.addmm(b, x.reshape(B * T, -1), wih.t()).view(B, T, 2, 4 * lstm.hidden_size)
+        x = _lib.lstm_bidir_layer(xp, whh, B, T)
+    return x
+
+
 class PyanNet(torch.nn.Module):
     """pyannote/segmentation's PyanNet (pyannote.audio PyanNet defaults, module names as in its
     checkpoints): SincNet (stride 10) -> BiLSTM(128, 2 layers, batch-first) -> 2 x (Linear(128)
@@ -316,7 +358,7 @@ class PyanNet(torch.nn.Module):
 
     def head(self, x: torch.Tensor) -> torch.Tensor:
         """LSTM -> linear layers -> classifier on the SincNet features [B, 60, frames]."""
-        x, _ = self.lstm(x.transpose(1, 2))
+        x = lstm_forward(self.lstm, x.transpose(1, 2))
         for lin in self.linear:
             x = F.leaky_relu(lin(x))
         return torch.sigmoid(self.classifier(x))
