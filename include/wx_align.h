@@ -303,6 +303,15 @@ int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t
  * where chunk c's first frame lands (non-decreasing).  out[f] = (sum over covering chunks, in
  * chunk order, of max_k scores[c, f - start_frame[c], k]) / (number of them), NaN outputs
  * masked out; `missing` where no chunk covers f.  Feeds wx_binarize on the device. */
+/* VAD producer (vad.py:198-240 -> pyannote SincNet's stages 2 and 3): Conv1d(Cin, Cout, K)
+ * with no padding and stride 1 over every window of a time-major batch x [B][L][Cin]
+ * (contiguous, 16-byte aligned, Cin % 4 == 0, Cin <= 80, Cout <= 64, K == 5):
+ * y[b][t][o] = bias[o] + sum_{j<K, i<Cin} x[b][t + j][i] w[o][i][j], y [B][L - K + 1][Cout].
+ * w_packed [K][CINP / 4][64][4] (CINP = 64 for Cin <= 64, else 80), zero-padded:
+ * w_packed[j][i / 4][o][i % 4] = w[o][i][j].  fp32 (f32 MFMA: tolerance-equal to the GEMM route). */
+int wx_conv1d_taps_tm(const float* x, int64_t B, int64_t L, int32_t Cin, const float* w_packed, const float* bias,
+                      int32_t Cout, int32_t K, float* y, void* stream);
+
 /* VAD producer (vad.py:198-240 -> pyannote PyanNet's LSTM): one bidirectional LSTM layer,
  * hidden size H = 128, over B sequences of T steps, both directions in one persistent launch.
  * xp [B][T][2][4H]: each step's input projection x W_ih^T + b_ih + b_hh per direction (gate

@@ -244,3 +244,23 @@ def test_lstm_kernel_producer_scores_and_chunks(monkeypatch):
     thr = float(0.5 * (vals[i] + vals[i + 1]))
     assert vals[i + 1] - vals[i] > 4 * diff
     assert merge_chunks(feat_k, 30, onset=thr, offset=thr) == merge_chunks(feat_p, 30, onset=thr, offset=thr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,Cin,Cout", [(3, 2658, 80, 60), (5, 884, 60, 60), (2, 5, 80, 60), (1, 300, 8, 4),
+                                         (7, 129, 64, 64)])
+def test_conv_taps_kernel_vs_torch(B, L, Cin, Cout):
+    """wx_conv1d_taps_tm (SincNet's k = 5 convolutions, every window in one launch) through
+    vad_model.conv1d_batched against torch's fp32 conv1d: both PyanNet stage shapes, a single
+    output frame, narrow channels, the 128-frame tile edge."""
+    from whisperx_amd import vad_model
+
+    torch.manual_seed(B * L + Cin)
+    x_tm = torch.randn(B, L, Cin, device="cuda")
+    w = torch.randn(Cout, Cin, 5, device="cuda") * 0.1
+    b = torch.randn(Cout, device="cuda")
+    with torch.inference_mode():
+        ref = torch.nn.functional.conv1d(x_tm.transpose(1, 2), w, b)
+        got = vad_model.conv1d_batched(x_tm.transpose(1, 2), w, b, 1)
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)

@@ -83,6 +83,7 @@ SIGNATURES = {
     "wx_sincnet_stage_ex": (ctypes.c_int, [_vp, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp]),
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
+    "wx_conv1d_taps_tm": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
     "wx_lstm_bidir_layer": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "wx_posconv_packed": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
     "wx_attention_f32_packed": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
@@ -562,6 +563,21 @@ def sincnet_stage(x_tm: torch.Tensor, do_abs: bool, gamma, beta, eps: float, slo
     with torch.cuda.device(x_tm.device):
         _check(lib.wx_sincnet_stage_ex(_ptr(x_tm), B, L, C, int(x_tm.stride(0)), int(bool(do_abs)), _ptr(sc), _ptr(sh),
                                        _ptr(g), _ptr(bt), float(eps), float(slope), _ptr(y), _stream(x_tm.device)))
+    return y
+
+
+def conv1d_taps_tm(x_tm: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, k: int) -> torch.Tensor:
+    """wx_conv1d_taps_tm: Conv1d(Cin, cout, k) (no padding, stride 1) of every window of a
+    time-major [B, L, Cin] fp32 batch (contiguous) with the packed weights
+    [k][CINP / 4][64][4]; returns [B, L - k + 1, cout] time-major."""
+    lib = load()
+    B, L, C = (int(v) for v in x_tm.shape)
+    if not x_tm.is_contiguous() or x_tm.dtype != torch.float32:
+        raise WXError("conv1d_taps_tm: x must be a contiguous fp32 [B, L, Cin] tensor")
+    y = torch.empty((B, max(L - k + 1, 0), cout), dtype=torch.float32, device=x_tm.device)
+    with torch.cuda.device(x_tm.device):
+        _check(lib.wx_conv1d_taps_tm(_ptr(x_tm), B, L, C, _ptr(w_packed), _ptr(bias) if bias is not None else None,
+                                     int(cout), int(k), _ptr(y), _stream(x_tm.device)))
     return y
 
 

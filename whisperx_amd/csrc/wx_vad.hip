@@ -121,6 +121,103 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// SincNet's k = 5 convolutions (pyannote SincNet stages 2 and 3: Conv1d(80, 60, 5) and
+// Conv1d(60, 60, 5), no padding), time-major, every window of a batch in one launch.  As tap
+// GEMMs (vad_model.conv1d_batched) each was 5 passes over the [B L, Cin] activation with the
+// [B L, 60] output read and written per tap (memory-bound, ~33 ms per hour of audio).  Here
+// one block per (window, 128 output frames): the 132 input rows sit in LDS once, the taps'
+// [Cin, 64] weight slabs stream through a double-buffered LDS slab, 4 waves x 32 frames x 64
+// outputs (60 used) on v_mfma_f32_16x16x4_f32; + bias, written once.  fp32 (fma chains: not
+// bit-identical to the GEMM route, tests compare at fp32 tolerance).
+constexpr int kCkFrames = 128;
+
+template <int CINP, int KT>
+__global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict__ x, int Cin, int L,
+                                                        const float* __restrict__ wp /* [KT][CINP/4][64][4] */,
+                                                        const float* __restrict__ bias, float* __restrict__ y,
+                                                        int Cout, int Lout) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    constexpr int RS = CINP + 4;
+    constexpr int WR = kCkFrames + KT - 1;
+    constexpr int NOB = 4, NIC = CINP / 16;
+    constexpr int NB4 = CINP * 64 / 4;
+    constexpr int PER = (NB4 + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float xa[WR * RS];
+    __shared__ __attribute__((aligned(16))) float wb[2][CINP * 64];
+    const int b = blockIdx.y;
+    const int t0 = blockIdx.x * kCkFrames;
+    const float* xb = x + (int64_t)b * L * Cin;
+    const int c4n = Cin / 4;
+    for (int e = threadIdx.x; e < WR * (CINP / 4); e += 256) {
+        const int r = e / (CINP / 4), c4 = e - r * (CINP / 4);
+        const int t = t0 + r;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t < L && c4 < c4n) v = *reinterpret_cast<const float4*>(xb + (int64_t)t * Cin + 4 * c4);
+        *reinterpret_cast<float4*>(xa + r * RS + 4 * c4) = v;
+    }
+    const float4* wg = reinterpret_cast<const float4*>(wp);
+    float4 breg[PER];
+#define WX_CT_BLOAD(j) \
+    _Pragma("unroll") for (int p = 0; p < PER; ++p) breg[p] = wg[(int64_t)(j) * NB4 + min((int)threadIdx.x + 256 * p, NB4 - 1)];
+#define WX_CT_BSTORE(buf)                                                                 \
+    _Pragma("unroll") for (int p = 0; p < PER; ++p) if ((int)threadIdx.x + 256 * p < NB4) \
+        reinterpret_cast<float4*>(wb[buf])[threadIdx.x + 256 * p] = breg[p];
+    WX_CT_BLOAD(0)
+    WX_CT_BSTORE(0)
+    __syncthreads();
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
+    f32x4 acc[2][NOB];
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) acc[fb][ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* xrow = xa + (wv * 32 + r16) * RS + 4 * q;
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        if (j + 1 < KT) {
+            WX_CT_BLOAD(j + 1)
+        }
+        const float* bb = wb[j & 1] + (q * 64 + r16) * 4;
+#pragma unroll
+        for (int ic = 0; ic < NIC; ++ic) {
+            float4 av[2], bv[NOB];
+#pragma unroll
+            for (int fb = 0; fb < 2; ++fb) av[fb] = *reinterpret_cast<const float4*>(xrow + (16 * fb + j) * RS + 16 * ic);
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) bv[ob] = *reinterpret_cast<const float4*>(bb + (ic * 4 * 64 + 16 * ob) * 4);
+#pragma unroll
+            for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+                for (int ob = 0; ob < NOB; ++ob) {
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].x, bv[ob].x, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].y, bv[ob].y, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].z, bv[ob].z, acc[fb][ob], 0, 0, 0);
+                    acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].w, bv[ob].w, acc[fb][ob], 0, 0, 0);
+                }
+        }
+        if (j + 1 < KT) {
+            WX_CT_BSTORE((j + 1) & 1)
+        }
+        __syncthreads();
+    }
+#undef WX_CT_BLOAD
+#undef WX_CT_BSTORE
+    float* yb = y + (int64_t)b * Lout * Cout;
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int t = t0 + wv * 32 + 16 * fb + 4 * q + v;
+            if (t >= Lout) continue;
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) {
+                const int c = 16 * ob + r16;
+                if (c < Cout) yb[(int64_t)t * Cout + c] = acc[fb][ob][v] + (bias ? bias[c] : 0.f);
+            }
+        }
+}
+
+// ------------------------------------------------------------------------------------
 // PyanNet's bidirectional LSTM layer (pyannote segmentation, called by vad.py:198-240), one
 // persistent kernel per layer for both directions.  MIOpen ran it as 293 time steps x 2
 // directions of a [B, 128] x [128, 512] GEMM launch plus a gate-update launch (~37 k launches
@@ -266,6 +363,27 @@ extern "C" int wx_lstm_bidir_layer(const float* xp, const float* whh, float* y, 
     const dim3 grid((unsigned)((B + kLR - 1) / kLR), 2);
     hipLaunchKernelGGL(lstm_layer_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xp, whh, y,
                        (int)B, (int)T);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_conv1d_taps_tm(const float* x, int64_t B, int64_t L, int32_t Cin, const float* w_packed,
+                                 const float* bias, int32_t Cout, int32_t K, float* y, void* stream) {
+    using namespace wxv;
+    if (B < 0 || L < 0 || Cin <= 0 || (Cin & 3) || Cout <= 0 || Cout > 64 || !x || !w_packed || !y) return WX_E_INVALID;
+    const int64_t Lout = L >= K ? L - K + 1 : 0;
+    if (B == 0 || Lout == 0) return WX_OK;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) || B > 65535 || L > INT32_MAX) return WX_E_INVALID;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)((Lout + kCkFrames - 1) / kCkFrames), (unsigned)B);
+    if (K == 5 && Cin <= 64)
+        hipLaunchKernelGGL((conv_taps_kernel<64, 5>), grid, dim3(256), 0, s, x, Cin, (int)L, w_packed, bias, y, Cout,
+                           (int)Lout);
+    else if (K == 5 && Cin <= 80)
+        hipLaunchKernelGGL((conv_taps_kernel<80, 5>), grid, dim3(256), 0, s, x, Cin, (int)L, w_packed, bias, y, Cout,
+                           (int)Lout);
+    else
+        return WX_E_INVALID;
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

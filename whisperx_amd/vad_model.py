@@ -108,6 +108,28 @@ class SincFilterbank(torch.nn.Module):
 _PATCH_BYTES = int(os.environ.get("WX_VAD_PATCH_MB", "1024")) << 20  # conv1d_batched: patch buffer per chunk of windows (Cin == 1)
 
 
+_CT_CACHE: dict = {}
+
+
+def _conv_taps_weights(w: torch.Tensor) -> torch.Tensor:
+    """w [Cout, Cin, k] packed for wx_conv1d_taps_tm ([k][CINP / 4][64][4], zero-padded),
+    cached per weight tensor (identity and version)."""
+    ver = w._version if not w.is_inference() else -1
+    hit = _CT_CACHE.get(id(w))
+    c = hit[2] if hit is not None and hit[0]() is w and hit[1] == ver else None
+    if c is None:
+        Cout, Cin, k = w.shape
+        cinp = 64 if Cin <= 64 else 80
+        with torch.no_grad():
+            wp = torch.zeros((k, cinp, 64), dtype=torch.float32, device=w.device)
+            wp[:, :Cin, :Cout] = w.detach().permute(2, 1, 0)
+            c = wp.view(k, cinp // 4, 4, 64).permute(0, 1, 3, 2).contiguous()
+        if len(_CT_CACHE) > 16:
+            _CT_CACHE.clear()
+        _CT_CACHE[id(w)] = (weakref.ref(w), ver, c)  # (the weakref: an id reused by another tensor misses)
+    return c
+
+
 def conv1d_batched(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride: int) -> torch.Tensor:
     """F.conv1d(x, w, b, stride) (no padding, dilation 1, one group) for a batch of windows
     through a few large GEMMs.  MIOpen's choice for these shapes depends on the state of its
@@ -145,7 +167,14 @@ def conv1d_batched(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
                 torch.mm(p, wp, out=o)
         return out.transpose(1, 2)
     assert stride == 1
-    X = x.transpose(1, 2).reshape(B * L, Cin)  # time-major copy
+    xt = x.transpose(1, 2)
+    if (not os.environ.get("WX_NO_CONV_KERNEL") and x.is_cuda and k == 5 and Cout <= 64 and Cin <= 80 and Cin % 4 == 0
+            and xt.is_contiguous() and x.dtype == torch.float32 and xt.data_ptr() % 16 == 0 and B <= 65535):
+        # every window's conv in one kernel (wx_conv1d_taps_tm): the activation read once
+        from . import _lib
+
+        return _lib.conv1d_taps_tm(xt, _conv_taps_weights(w), b, Cout, k).transpose(1, 2)
+    X = xt.reshape(B * L, Cin)  # time-major copy
     R = B * L - k + 1
     full = torch.empty((B * L, Cout), dtype=x.dtype, device=x.device)
     wt = w.permute(2, 1, 0)  # [k, Cin, Cout]
