@@ -172,19 +172,20 @@ def _packed_vs_per_segment(m, V, lengths, tol=5e-5):
                                  -1)[0] for w in wavs]
     streams = [torch.cuda.Stream() for _ in range(3)]
     worst = 0.0
-    with emission.prepared(m):
-        emission.materialize_weights(m)
-        assert emission.packed_supported(m)
-        Ts = [emission.n_frames(n, m) for n in lengths]
-        with torch.inference_mode():
-            got = torch.log_softmax(emission.packed_logits(m, wavs, _lib.PackedSegments(Ts), streams), -1)
-        torch.cuda.synchronize()
-        # and through _emissions (pack ranges, CSR rows, events)
-        csr = alignment._emissions(m, "huggingface", wavs, "cuda:0", n_streams=3)
-        main = torch.cuda.current_stream()
-        for st in csr.streams:
-            main.wait_stream(st)
-        torch.cuda.synchronize()
+    # the packed route runs the unprepared model from its weights (no patched forward)
+    assert emission.packed_supported(m) and not getattr(m, "_wx_gemm_conv", False)
+    Ts = [emission.n_frames(n, m) for n in lengths]
+    with torch.inference_mode():
+        got = torch.log_softmax(emission.packed_logits(m, wavs, _lib.PackedSegments(Ts), streams), -1)
+    torch.cuda.synchronize()
+    # and through _emissions (pack ranges, CSR rows, events)
+    csr = alignment._emissions(m, "huggingface", wavs, "cuda:0", n_streams=3)
+    assert isinstance(csr, alignment._EmissionsCSR) and csr.groups, "the packed route was not taken"
+    main = torch.cuda.current_stream()
+    for st in csr.streams:
+        main.wait_stream(st)
+    torch.cuda.synchronize()
+    assert not any("forward" in mod.__dict__ for mod in m.modules()), "the packed route patched the model"
     off = np.cumsum([0] + Ts)
     for i, r in enumerate(ref):
         g = got[off[i]: off[i + 1]]

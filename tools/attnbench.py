@@ -35,7 +35,37 @@ def run(H, streams, iters=50):
     return dt, fl / dt / 1e12, err
 
 
+def run_packed(H, nseg, split, iters=20):
+    """wx_attention_f32_packed on the packed encoder's layout: nseg segments of 1499 rows in one
+    fused [1, R, 3 H 64] q/k/v projection (views), one launch."""
+    import whisperx_amd._lib as L
+    dev = torch.device("cuda", 0)
+    segs = L.PackedSegments([1499] * nseg)
+    R = segs.rows
+    qkv = torch.randn(1, R, 3 * H * 64, device=dev)
+    q, k, v = (qkv[..., i * H * 64:(i + 1) * H * 64].view(1, R, H, 64).transpose(1, 2) for i in range(3))
+    for _ in range(5):
+        L.attention_f32_packed(q, k, v, 0.125, segs, split)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        L.attention_f32_packed(q, k, v, 0.125, segs, split)
+    e1.record()
+    torch.cuda.synchronize()
+    dt = e0.elapsed_time(e1) / 1e3 / iters
+    fl = 4 * H * 1499 * 1499 * 64 * nseg
+    return dt, fl / dt / 1e12
+
+
 if __name__ == "__main__":
+    if os.environ.get("ATTN_PACKED"):  # ATTN_PACKED=12 python tools/attnbench.py: packed launches, this library
+        n = int(os.environ["ATTN_PACKED"])
+        run_packed(12, n, 0)
+        for sp in (1, 2, 4):
+            dt, tf = run_packed(12, n, sp)
+            print(f"packed H=12 segments={n} split={sp}: {dt*1e6:8.1f} us/call {tf:6.1f} TFLOP/s", flush=True)
+        sys.exit(0)
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", required=True)
     ap.add_argument("--child", action="store_true")

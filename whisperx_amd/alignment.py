@@ -297,7 +297,9 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda":
         return [_emission(model, model_type, w, device) for w in waveforms]
-    if not os.environ.get("WX_MIOPEN_CONV"):
+    packed = (not os.environ.get("WX_MIOPEN_CONV") and model_type == "huggingface"
+              and emission.packed_supported(model))
+    if not os.environ.get("WX_MIOPEN_CONV") and not packed:
         emission.prepare_model(model)
         # cached weight_norm weights are built here, on the current stream, before the
         # side streams wait on it (a lazily built cache would race between the streams)
@@ -318,7 +320,7 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
         _EMISSION_STREAMS[key] = streams
     for st in streams:
         st.wait_stream(main)
-    if model_type == "huggingface" and emission.packed_supported(model):
+    if packed:
         try:
             csr.groups = _pack_ranges(Ts)
             csr.events = _packed_emissions(model, waveforms, csr, streams)
@@ -470,7 +472,10 @@ def align(
     # the model is prepared (GEMM convolutions, wx attention) for this call only: the caller's
     # model is restored when align() returns, after every forward has been joined
     gpu_route = torch.device(device).type == "cuda" and not os.environ.get("WX_MIOPEN_CONV")
-    with emission.prepared(model) if gpu_route else contextlib.nullcontext():
+    # the packed encoder runs the model from its weights: no forward is patched, so the model
+    # is not prepared (prepare + restore cost ~5 ms of host time per call before the first kernel)
+    packed = gpu_route and model_type == "huggingface" and emission.packed_supported(model)
+    with emission.prepared(model) if gpu_route and not packed else contextlib.nullcontext():
         with _Phase("emission"):
             ems = _emissions(model, model_type, wavs, device)
 

@@ -241,7 +241,6 @@ def _patched_forward(self, x):
 
 
 _ATTN_NAME = "wx_f32"
-_PACK = threading.local()  # .segs: the PackedSegments of the packed encoder running on this thread
 _PACK_SPLIT = int(os.environ.get("WX_ATTN_PACKED_SPLIT", "0"))  # waves per query tile (0: by size)
 
 
@@ -258,10 +257,6 @@ def _wx_attention(module, query, key, value, attention_mask, dropout: float = 0.
         from . import _lib
 
         scale = scaling if scaling is not None else query.shape[-1] ** -0.5
-        segs = getattr(_PACK, "segs", None)
-        if segs is not None and query.shape[0] == 1 and query.shape[2] == segs.rows:
-            # the packed encoder (packed_logits): each segment attends only to its own rows
-            return _lib.attention_f32_packed(query, key, value, scale, segs, _PACK_SPLIT), None
         return _lib.attention_f32(query, key, value, scale), None
     return _orig_attention(module)(module, query, key, value, attention_mask, dropout=dropout, scaling=scaling,
                                    **kwargs)
@@ -307,11 +302,13 @@ def _use_wx_attention(model: torch.nn.Module) -> None:
 _QKV_TLS = threading.local()  # the fused projection's k / v results until k_proj / v_proj take them
 
 
-def _qkv_weights(q: torch.nn.Linear):
+def _qkv_weights(q: torch.nn.Linear, k: Optional[torch.nn.Linear] = None, v: Optional[torch.nn.Linear] = None):
     """The attention's [Wq; Wk; Wv] (and biases) concatenated, cached until a parameter
-    changes (filled by materialize_weights on the caller's stream before any fan-out)."""
-    st = q.__dict__["_wx_qkv"]
-    k, v = st["k"], st["v"]
+    changes (filled by materialize_weights on the caller's stream before any fan-out).  k / v
+    default to the projections _fuse_qkv paired with q."""
+    if k is None:
+        st = q.__dict__["_wx_qkv"]
+        k, v = st["k"], st["v"]
     params = [m.weight for m in (q, k, v)] + [m.bias for m in (q, k, v) if m.bias is not None]
     key = tuple((p.data_ptr(), p._version) for p in params)
     c = _QKV_CACHE.get(q)
@@ -541,29 +538,48 @@ def log_softmax_into(logits: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 _PACK_ENCODERS = ("Wav2Vec2Encoder", "Wav2Vec2EncoderStableLayerNorm")
 
 
+def _layer_ok(layer, D: int) -> bool:
+    """A transformers Wav2Vec2 encoder layer the packed encoder can run from its weights: q/k/v/out
+    Linears with biases, head size 64, LayerNorms of width D, a feed-forward of two Linears."""
+    att = getattr(layer, "attention", None)
+    ff = getattr(layer, "feed_forward", None)
+    lins = [getattr(att, n, None) for n in ("q_proj", "k_proj", "v_proj", "out_proj")]
+    if (att is None or ff is None or not all(isinstance(m, torch.nn.Linear) and m.bias is not None for m in lins)
+            or getattr(att, "head_dim", 0) != 64 or getattr(att, "is_causal", False)
+            or getattr(layer, "adapter_layer", None) is not None):
+        return False
+    norms = (getattr(layer, "layer_norm", None), getattr(layer, "final_layer_norm", None))
+    return (all(isinstance(n, torch.nn.LayerNorm) and tuple(n.normalized_shape) == (D,) and n.weight is not None
+                and n.bias is not None for n in norms)
+            and isinstance(getattr(ff, "intermediate_dense", None), torch.nn.Linear)
+            and isinstance(getattr(ff, "output_dense", None), torch.nn.Linear))
+
+
 def packed_supported(model: torch.nn.Module) -> bool:
-    """Whether packed_logits can run this model: a prepared (prepare_model) transformers
-    Wav2Vec2ForCTC-shaped model in eval mode whose attention is wx_attention_f32, without
-    adapters (WX_NO_PACKED=1: never)."""
-    if os.environ.get("WX_NO_PACKED") or model.training or not getattr(model, "_wx_gemm_conv", False):
+    """Whether packed_logits can run this model: a transformers Wav2Vec2ForCTC-shaped model in
+    eval mode (no adapters) whose feature encoder, positional conv and encoder layers the
+    packed encoder runs from their weights (WX_NO_PACKED=1: never).  The model needs no
+    prepare_model: the packed path calls no patched forward."""
+    if os.environ.get("WX_NO_PACKED") or model.training:
         return False
     w2v = getattr(model, "wav2vec2", None)
     head = getattr(model, "lm_head", None)
     if w2v is None or not isinstance(head, torch.nn.Linear) or getattr(w2v, "adapter", None) is not None:
         return False
     enc = getattr(w2v, "encoder", None)
-    cfg = getattr(model, "config", None)
-    if (type(enc).__name__ not in _PACK_ENCODERS or cfg is None or getattr(cfg, "_attn_implementation", None) != _ATTN_NAME
-            or not hasattr(w2v, "feature_extractor") or not hasattr(w2v, "feature_projection")
-            or not hasattr(enc, "pos_conv_embed")):
+    fp = getattr(w2v, "feature_projection", None)
+    if (type(enc).__name__ not in _PACK_ENCODERS or fp is None or not hasattr(w2v, "feature_extractor")
+            or not hasattr(enc, "pos_conv_embed") or _fe_layers(w2v.feature_extractor) is None
+            or _posconv_weights(enc.pos_conv_embed, probe=True) is None):
         return False
-    return all(getattr(layer, "adapter_layer", None) is None for layer in enc.layers)
+    D = getattr(getattr(enc, "layer_norm", None), "normalized_shape", (0,))[0]
+    return D in _ADDLN_WIDTHS and all(_layer_ok(layer, D) for layer in enc.layers)
 
 
 _PC_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
-def _posconv_weights(pce):
+def _posconv_weights(pce, probe: bool = False):
     """(w_packed, bias, G, K) for wx_posconv_packed when the positional conv embedding is
     wav2vec2's (Conv1d K = 128, padding 64, G groups of 48 or 64 channels, the last output
     dropped, erf GELU), else None.  w_packed [G][K][Cg / 4][Cg][4] is cached per module until
@@ -579,6 +595,8 @@ def _posconv_weights(pce):
     D = conv.out_channels
     if conv.in_channels != D or D % G or D // G not in (48, 64):
         return None
+    if probe:
+        return True
     w = _weight(conv)
     key = (w.data_ptr(), _version(w)) + tuple((t.data_ptr(), _version(t)) for t in conv.parameters())
     c = _PC_CACHE.get(conv)
@@ -614,13 +632,34 @@ def _packed_encoder(enc, h: torch.Tensor, segs) -> torch.Tensor:
             h = _lib.add_layernorm(h, pos, ln.weight, ln.bias, ln.eps)
         else:
             h = ln(h + pos)
-    _PACK.segs = segs
-    try:
-        for layer in enc.layers:
-            h = layer(h, attention_mask=None)[0]
-    finally:
-        _PACK.segs = None
+    for layer in enc.layers:
+        h = _packed_layer(layer, h, segs, stable)
     return ln(h) if stable else h
+
+
+def _packed_layer(layer, h: torch.Tensor, segs, stable: bool) -> torch.Tensor:
+    """Wav2Vec2EncoderLayer (post-norm) / Wav2Vec2EncoderLayerStableLayerNorm (pre-norm) of an
+    eval forward over packed rows h [1, R, D], from the layer's weights: one q/k/v GEMM,
+    per-segment attention (wx_attention_f32_packed), the output projection, each
+    `norm(residual + x)` as one wx_add_layernorm."""
+    from . import _lib
+
+    att = layer.attention
+    ln, fln = layer.layer_norm, layer.final_layer_norm
+    R, D = h.shape[1], h.shape[2]
+    H = D // 64
+    w, b = _qkv_weights(att.q_proj, att.k_proj, att.v_proj)
+    x = ln(h) if stable else h
+    qkv = F.linear(x, w, b)  # [1, R, 3D]
+    q, k, v = (qkv[..., i * D:(i + 1) * D].view(1, R, H, 64).transpose(1, 2) for i in range(3))
+    scale = getattr(att, "scaling", None) or 64 ** -0.5
+    o = _lib.attention_f32_packed(q, k, v, scale, segs, _PACK_SPLIT).reshape(1, R, D)
+    o = att.out_proj(o)
+    if stable:
+        y, s = _lib.add_layernorm(h, o, fln.weight, fln.bias, fln.eps, want_sum=True)
+        return s + layer.feed_forward(y)
+    h1 = _lib.add_layernorm(h, o, ln.weight, ln.bias, ln.eps)
+    return _lib.add_layernorm(h1, layer.feed_forward(h1), fln.weight, fln.bias, fln.eps)
 
 
 _FE_KINDS = {"Wav2Vec2GroupNormConvLayer": "group", "Wav2Vec2LayerNormConvLayer": "layer",
