@@ -65,10 +65,10 @@ def test_pack_ranges():
     assert alignment._pack_ranges([4, 4, 4], 10) == [(0, 2), (2, 3)]
     assert alignment._pack_ranges([12, 1, 9, 1], 10) == [(0, 1), (1, 3), (3, 4)]
     assert alignment._pack_ranges([5, 5], 10) == [(0, 2)]
-    # a last pack of >= 4 segments leaves its last quarter to a pack of its own
-    assert alignment._pack_ranges([1499] * 16, 49152) == [(0, 12), (12, 16)]
+    # a last pack of >= 8 segments leaves its last eighth to a pack of its own
+    assert alignment._pack_ranges([1499] * 16, 49152) == [(0, 14), (14, 16)]
     assert alignment._pack_ranges([1] * 9, 6) == [(0, 6), (6, 9)]
-    assert alignment._pack_ranges([1] * 10, 6) == [(0, 6), (6, 9), (9, 10)]
+    assert alignment._pack_ranges([1] * 20, 12) == [(0, 12), (12, 19), (19, 20)]
 
 
 def test_packed_segments_layout():

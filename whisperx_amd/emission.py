@@ -555,13 +555,32 @@ def _layer_ok(layer, D: int) -> bool:
             and isinstance(getattr(ff, "output_dense", None), torch.nn.Linear))
 
 
+_SUPPORT_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
 def packed_supported(model: torch.nn.Module) -> bool:
     """Whether packed_logits can run this model: a transformers Wav2Vec2ForCTC-shaped model in
     eval mode (no adapters) whose feature encoder, positional conv and encoder layers the
     packed encoder runs from their weights (WX_NO_PACKED=1: never).  The model needs no
-    prepare_model: the packed path calls no patched forward."""
+    prepare_model: the packed path calls no patched forward.  The structural check is cached
+    per model (keyed on its encoder and layer list: ~0.4 ms of host time per call otherwise)."""
     if os.environ.get("WX_NO_PACKED") or model.training:
         return False
+    enc = getattr(getattr(model, "wav2vec2", None), "encoder", None)
+    layers = getattr(enc, "layers", None)
+    n = (id(enc), id(layers), len(layers) if layers is not None else -1)
+    hit = _SUPPORT_CACHE.get(model)
+    if hit is not None and hit[0] == n:
+        return hit[1]
+    ok = _packed_structure_ok(model)
+    try:
+        _SUPPORT_CACHE[model] = (n, ok)
+    except TypeError:  # (a model that cannot be weakly referenced: not cached)
+        pass
+    return ok
+
+
+def _packed_structure_ok(model: torch.nn.Module) -> bool:
     w2v = getattr(model, "wav2vec2", None)
     head = getattr(model, "lm_head", None)
     if w2v is None or not isinstance(head, torch.nn.Linear) or getattr(w2v, "adapter", None) is not None:
