@@ -720,15 +720,26 @@ def _tm_conv(conv: torch.nn.Conv1d, x: torch.Tensor, Lout: int) -> torch.Tensor:
         return torch.addmm(b, patches, w) if b is not None else torch.mm(patches, w)
     wt = _tap_weights(conv)  # [k, Cin, Cout]
     out = torch.empty((Lout, Cout), dtype=x.dtype, device=x.device)
-    for j in range(k):
-        xj = x[j: j + s * (Lout - 1) + 1: s]
-        if j == 0:
+    Cin = conv.in_channels
+    if os.environ.get("WX_FE_TAPS"):  # (A/B: one GEMM per tap)
+        groups = [(j, 1) for j in range(k)]
+        rs = s * Cin
+    else:
+        # taps s g .. s g + s - 1 read s consecutive rows of x: one contiguous s Cin-wide row of
+        # the view with row stride s Cin, so they are ONE GEMM with K = s Cin (k = 3, s = 2: two
+        # GEMMs, K = 1024 and 512, instead of three; k = 2, s = 2: one GEMM, no accumulation)
+        groups = [(j, min(s, k - j)) for j in range(0, k, s)]
+        rs = s * Cin
+    for n, (j, r) in enumerate(groups):
+        xj = x.as_strided((Lout, r * Cin), (rs, 1), x.storage_offset() + j * Cin)
+        wj = wt[j:j + r].reshape(r * Cin, Cout)
+        if n == 0:
             if b is not None:
-                torch.addmm(b, xj, wt[0], out=out)
+                torch.addmm(b, xj, wj, out=out)
             else:
-                torch.mm(xj, wt[0], out=out)
+                torch.mm(xj, wj, out=out)
         else:
-            out.addmm_(xj, wt[j])
+            out.addmm_(xj, wj)
     return out
 
 
