@@ -262,17 +262,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int i = 0; i < 8; ++i) c[i] = 0.f;
     __syncthreads();
-    for (int s = 0; s < T; ++s) {
+    // xp rows of a step: accumulator (tile, v) <-> row 4 q + v, column 16 tile + r16 of gate w;
+    // the next step's are loaded while this step's MFMAs run
+    float xn[8][4];
+    auto load_xp = [&](int s) {
         const int t = d ? T - 1 - s : s;
-        f32x4 acc[8];
-        // xp rows of this step: accumulator (tile, v) <-> row 4 q + v, column 16 tile + r16 of gate w
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const int b = min(b0 + 4 * q + v, B - 1);
             const float* xr = xp + (((int64_t)b * T + t) * 2 + d) * 4 * kLH + 128 * w + r16;
 #pragma unroll
-            for (int tile = 0; tile < 8; ++tile) acc[tile][v] = xr[16 * tile];
+            for (int tile = 0; tile < 8; ++tile) xn[tile][v] = xr[16 * tile];
         }
+    };
+    load_xp(0);
+    for (int s = 0; s < T; ++s) {
+        const int t = d ? T - 1 - s : s;
+        f32x4 acc[8];
+#pragma unroll
+        for (int tile = 0; tile < 8; ++tile)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[tile][v] = xn[tile][v];
+        if (s + 1 < T) load_xp(s + 1);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             const float4 a = *reinterpret_cast<const float4*>(hs + r16 * RS + 16 * kk + 4 * q);
