@@ -442,6 +442,56 @@ __device__ __forceinline__ uint64_t granule_load(const uint64_t* g) {
     return __hip_atomic_load(const_cast<uint64_t*>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Split segments publish their decision words and column-N history write-through (WT: sc1
+// stores, which leave the XCD's L2 at once) and the last part to arrive reads them with sc1
+// loads, L1-bypassing: the arrival then needs neither the release fence (buffer_wbl2: the
+// write-back of every dirty line of the XCD's L2, ~2-6 us behind a part's freshly written
+// bits) nor the acquire (MI355X_MICROARCH.md, "Valid forms": one lane per storing workgroup
+// adds to one counter after every storing wave's vmcnt(0) wait and a workgroup barrier, the
+// workgroup whose add came last loads after it returned, its other waves after a barrier;
+// 4- and 16-byte sc1 stores and loads).  -DWX_SPLIT_FENCED builds the fenced protocol.
+#ifdef WX_SPLIT_FENCED
+constexpr bool kSplitWT = false;
+#else
+constexpr bool kSplitWT = true;
+#endif
+// Register-resident split kernels only (C = 1, config 2): in the C > 1 split kernels the
+// consumer's hand-off waits drain vmcnt inside the chain, and write-through stores take longer
+// to drain (A/B, 64 x T = 2999, N ~ 900: fenced 166 us, write-through 178 us).
+template <int C, int VS, bool SP>
+constexpr bool split_wt() {
+    return SP && kSplitWT && C == 1 && VS != kGatherVS;
+}
+template <bool WT, class T>
+__device__ __forceinline__ T ld_pub(const T* p) {
+    if constexpr (WT)
+        return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dword sc1
+    else
+        return *p;
+}
+template <bool WT, class T>
+__device__ __forceinline__ void st_pub(T* p, T v) {
+    if constexpr (WT)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
+    else
+        *p = v;
+}
+// 16 bytes at base[i .. i + 3] (base wave-uniform).  WT: a buffer store with the sc1 bit (aux
+// 16), through the builtin so that the compiler keeps its hazard and vmcnt bookkeeping (an asm
+// dwordx4 store's data registers could be overwritten in the next instruction).
+template <bool WT>
+__device__ __forceinline__ void st_pub4(float* base, int i, float4 v) {
+    if constexpr (WT) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+        const u4 x = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y),
+                      __builtin_bit_cast(unsigned, v.z), __builtin_bit_cast(unsigned, v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, i * 4, 0, 16);
+    } else {
+        *reinterpret_cast<float4*>(base + i) = v;
+    }
+}
+
 template <int C, int W>
 struct Geometry {
     static constexpr int HL = W > 1 ? (32 + C - 1) / C : 0;  // halo lanes per wave >= 1
@@ -491,6 +541,7 @@ struct Forward {
     // LDS read, no wait.  Micro-benchmarks (tools/ubench/step*.hip): a step costs ~20 cycles
     // of one wave alone, each LDS read issued inside the chain ~9 more.
     static constexpr bool kReg = C == 1 && MODE == 0 && SP && NH == 2 && VS != kGatherVS;
+    static constexpr bool kWT = split_wt<C, VS, SP>();
     static constexpr int kBufFloats = kReg ? quad_buf_floats<VS>() : kChunk * VS;  // one chunk buffer
     static constexpr int kQS = quad_stride<VS>();
 
@@ -695,7 +746,7 @@ struct Forward {
         for (int k = 0; k < C; ++k) wdef[k] = 0u;
         auto store_deferred = [&](const int qd) {
 #pragma unroll
-            for (int k = 0; k < C; ++k) bits[((int64_t)qd * C + k) * lanes + g] = wdef[k];
+            for (int k = 0; k < C; ++k) st_pub<kWT>(bits + ((int64_t)qd * C + k) * lanes + g, wdef[k]);
         };
         // kReg: the operands of the chunk being computed (o) and of the next one (n), swapped
         // by the two-way unrolled chunk loop
@@ -950,12 +1001,12 @@ struct Forward {
             // land in the segment's padding (kCnPad).  (Stored per 8 steps inside the chain,
             // with a partial-group path, they cost the pacing wave a taken branch and an EXEC
             // round trip per 8 steps: 59.7 -> 55.3 -> ... us.)
-            // (Written through with sc1 stores — so that the arrival's release would have no
-            // dirty line to write back — the 32 single stores cost more than the release.)
-            float4* d4 = reinterpret_cast<float4*>(cn + t0);
+            // Eight 16-byte stores, written through (sc1, kWT): the last part reads them with
+            // sc1 loads and the arrival needs no release (32 single 4-byte sc1 stores had cost
+            // more than the release).
 #pragma unroll
             for (int i = 0; i < kChunk / 4; ++i)
-                d4[i] = make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]);
+                st_pub4<kWT>(cn, t0 + 4 * i, make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]));
         }
     }
     // tr[t][0] + em[t, tok[0]] for the rows of chunk q (the column-1 wave's lane-0 operand),
@@ -1348,10 +1399,9 @@ struct Forward {
                 }
             }
             if (MODE != 1 && owner) {  // rows t-kU+1 .. t at cn[t-kU .. t-1] (16-byte aligned)
-                float4* o = reinterpret_cast<float4*>(cn + st.t - kU);
 #pragma unroll
                 for (int i = 0; i < kU / 4; ++i)
-                    o[i] = make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]);
+                    st_pub4<kWT>(cn, st.t - kU + 4 * i, make_float4(hist[4 * i], hist[4 * i + 1], hist[4 * i + 2], hist[4 * i + 3]));
             }
         }
         for (; r < rows; ++r) {
@@ -1361,7 +1411,7 @@ struct Forward {
             for (int k = 0; k < C; ++k) ga[k] = gb + toff[k];
             step<!WAVE0 ? 0 : (kC0Lds ? kColLds : kColAny)>(gb, ga, 0, boff, c0q + r, st, inf_from, is_short, halo, f,
                                                        cnt, N, tr);
-            if (MODE != 1 && owner) cn[st.t] = st.cur[C - 1];
+            if (MODE != 1 && owner) st_pub<kWT>(cn + st.t, st.cur[C - 1]);
             ++st.t;
         }
     }
@@ -1415,9 +1465,8 @@ struct Forward {
             hist[u & (kUnroll - 1)] = st.cur[C - 1];
             ++st.t;
             if (MODE != 1 && (u & (kUnroll - 1)) == kUnroll - 1 && owner) {
-                float4* o = reinterpret_cast<float4*>(cn + st.t - kUnroll);
-                o[0] = make_float4(hist[0], hist[1], hist[2], hist[3]);
-                o[1] = make_float4(hist[4], hist[5], hist[6], hist[7]);
+                st_pub4<kWT>(cn, st.t - kUnroll, make_float4(hist[0], hist[1], hist[2], hist[3]));
+                st_pub4<kWT>(cn, st.t - kUnroll + 4, make_float4(hist[4], hist[5], hist[6], hist[7]));
             }
         }
     }
@@ -1518,6 +1567,7 @@ __device__ void fill_q0(const float* __restrict__ E, int V, int T, float* __rest
 
 // Argmax of column N over rows 0..T with torch.argmax semantics (first maximum; the first
 // NaN wins), rows 1..T read from cn[0..T-1], row 0 = -inf (alignment.py:395-396).  Wave 0.
+template <bool WT = false>  // WT: sc1 loads (a split segment's history, written through by another CU)
 __device__ int column_argmax(const float* __restrict__ cn, int T) {
     const int l = lane_id();
     int nan_row = 0x7fffffff, best_row = 0;
@@ -1528,7 +1578,7 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
             const int i = base + u * kWave + l;
-            v[u] = i < T ? cn[i] : -INFINITY;
+            v[u] = i < T ? ld_pub<WT>(cn + i) : -INFINITY;
         }
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {  // rows of a lane in increasing order
@@ -1676,7 +1726,7 @@ __device__ __noinline__ bool generic_forward(int T, int N, int blank, const floa
 // executed by the whole wave; `lay` maps cells to the bitmap's (lane, slot) words.
 // Records start[k] = first frame of token k (the frame where the path moved onto it).
 // Returns true on success (j reached 0), false where the reference returns None.
-template <int CC>
+template <int CC, bool WT = false>  // WT: sc1 loads (kSplitWT)
 __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bits, const Layout& lay, int b, int A) {
     // Unconditional (column clamped to 1, block to 0): the walk masks invalid lanes when it
     // uses the word, so the load can stay in flight across blocks (a conditional load
@@ -1687,7 +1737,7 @@ __device__ __forceinline__ unsigned load_window(const unsigned* __restrict__ bit
     const int jj = max(A - lane_id(), 1);
     int g, k;
     lay.locate<CC>(jj - 1, g, k);
-    return row[(unsigned)(k * lay.lanes + g)];
+    return ld_pub<WT>(row + (unsigned)(k * lay.lanes + g));
 }
 
 // Walk one 32-step block (decision indices 32b+31 .. 32b) from window offset d, run-length
@@ -1763,8 +1813,9 @@ __device__ __forceinline__ unsigned walk_block_rl(unsigned win, int& d) {
 // Decision words from the forward's bitmap (load_window): block bb's window issued at column
 // A holds columns A - lane (lo) and A - 64 - lane (hi); at use the 64 lanes from the walk's
 // offset are gathered (two ds_bpermutes, skipped while the block fits the first word).
-template <int CC>
+template <int CC, bool WT = false>  // WT: the words were written through by other CUs (kSplitWT)
 struct BitSrc {
+    static constexpr bool kWT = WT;
     const unsigned* bits;
     Layout lay;
     struct Win {
@@ -1773,8 +1824,8 @@ struct BitSrc {
     };
     __device__ __forceinline__ void issue(Win& w, int bb, int A) const {
         w.A = uniform(A);
-        w.lo = load_window<CC>(bits, lay, bb, A);
-        w.hi = load_window<CC>(bits, lay, bb, A - 64);
+        w.lo = load_window<CC, WT>(bits, lay, bb, A);
+        w.hi = load_window<CC, WT>(bits, lay, bb, A - 64);
     }
     __device__ __forceinline__ void end_block(int) const {}
     __device__ __forceinline__ void window(const Win& w, int b, int j, unsigned& win, int& dd) const {
@@ -1815,6 +1866,7 @@ struct BitSrc {
 // A - lane, A - 64 - lane, A - 128 - lane: the band of a block entered within 96 columns of A).
 template <int CC, int VS>
 struct CkSrc {
+    static constexpr bool kWT = false;
     const float* ck;      // checkpoint rows: tr[32q][j] at cell j's bitmap word of block q
     Layout lay;
     const double* acc;    // [q]: sum of em[0 .. 32q - 1, 0] in fp64 (column 0 before row 32q)
@@ -2193,7 +2245,7 @@ __device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn,
     unsigned fm0 = 0xFFFFFFFFu;
     int* rec = nullptr;
     if (wv == 0) {
-        t_start = column_argmax(cn, T);
+        t_start = column_argmax<Src::kWT>(cn, T);
         if (t_start <= 0) {
             res = -1;  // (the reference's None)
         } else {
@@ -2526,6 +2578,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // recompute every block serially: slower than the bits it saves), latency (helper), split
     // and gathered-vocabulary kernels keep the bitmap.
     constexpr bool CK = !SP && H == 0 && VS != kGatherVS && W >= 2;
+    constexpr bool WT = split_wt<C, VS, SP>();  // write-through hand-over of the bits to the last part
     // (CK: the walkers' row slots, one [32][VS] per wave, reuse the forward's buffers)
     constexpr int kLdsFloats = H ? (kLatencyLdsFloats > 4 * kChunk * VS ? kLatencyLdsFloats : 4 * kChunk * VS)
                                  : (CK ? kCkSlots<VS, W> : 2) * kChunk * VS;
@@ -2595,13 +2648,18 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     bool failed = false;
     if (SP && !slow) {  // release this part's bits / column-N history; the last part to arrive goes on
         if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            wait_vm();
+            // (WT: every wave's stores drained above, then the barrier: no release)
+            if (!WT) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                wait_vm();
+            }
             const unsigned w = split_arrive(a.arrive + seg, a.epoch, tsb[2] != 0);
             tsb[0] = ((w & 0x7Fu) == (unsigned)P) ? 1 + (int)((w >> 7) & 1u) : 0;
             if (tsb[0]) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                wait_vm();
+                if (!WT) {  // (WT: the walk reads the parts' words with sc1 loads)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    wait_vm();
+                }
                 // every part has arrived: leave the counter clean for the next launch
                 __hip_atomic_store(a.arrive + seg, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -2648,7 +2706,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if constexpr (W + H > 1) b_lo = walk_spec(wsrc, d.N, d.T, cn, cmask, lds_walk, K, colrec_lds, sbuf_lds, ts);
     if (lane < kWave) {  // wave 0: t_start, the walk, then the change masks -> start frames
         if constexpr (W + H == 1) {
-            ts = column_argmax(cn, d.T);
+            ts = column_argmax<WT>(cn, d.T);
             b_lo = walk_impl(wsrc, d.N, ts, cmask, lds_walk);
         }
         if (lane == 0) {
@@ -2694,7 +2752,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         wsrc.junk = xh;  // (the forward's halo exchange, free now: 2 W 64 floats >= 1 KB when W > 1)
         walk_tail(wsrc);
     } else {
-        BitSrc<C> wsrc{bits, lay};
+        BitSrc<C, WT> wsrc{bits, lay};
         walk_tail(wsrc);
     }
     wait_vm();
