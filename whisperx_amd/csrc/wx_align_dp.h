@@ -633,6 +633,11 @@ struct Forward {
             c0a = __shfl(a, kChunk);
         };
         if (c0prod && nch > 0) c0_make(0, c0_load(0));  // (before barrier 0)
+        if (H && wv >= W + NH) {  // split kernels' extra walker waves: keep the barrier count
+            if (kReg) __syncthreads();  // (barrier -1)
+            for (int q = 0; q < nch; ++q) __syncthreads();
+            return false;
+        }
         if (H && wv >= W) {
             // NH == 2 (split kernels): wave W stages, wave W + 1 runs column 0's fp64 chain;
             // one helper doing both paced part 0 (it reached every chunk barrier last)
@@ -2571,7 +2576,16 @@ constexpr int kCkSlots =
     (W == 1 || VS == 32) ? 2 * W : W;
 #endif
 
-template <int C, int VS, int W, int H, bool SP = false>
+// Split kernels: waves per workgroup.  Beyond the W DP waves and the two helpers, the rest
+// only keep the forward's barrier count and then walk speculative segments (walk_spec: more
+// walkers, shorter segments).  177 VGPRs allow two waves per SIMD: 8.  (-DWX_SPLIT_WAVES=6:
+// no extra walkers.)
+#ifndef WX_SPLIT_WAVES
+#define WX_SPLIT_WAVES 8
+#endif
+constexpr int kSplitWaves = WX_SPLIT_WAVES;
+
+template <int C, int VS, int W, int H, bool SP = false, int XW = 0>
 __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // Checkpointed forward (MODE 2, CkSrc walk): the single-CU throughput kernels with two or
     // more waves (speculative walkers) and staged row widths; the one-wave (a lone walker would
@@ -2588,7 +2602,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
     __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
-    __shared__ int sbuf_lds[3 * (W + H)];
+    __shared__ int sbuf_lds[3 * (W + H + XW)];
     __shared__ ColMapLds<VS> cml;
     __shared__ float xg_lds[SP && C == 1 ? 2 * 32 : 1];  // Split::xg
     const int P = SP ? a.parts : 1;
@@ -2696,7 +2710,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // wave (walk_spec, which also finds t_start); one wave walks alone
     const int nbw = ((d.T - 1) >> 5) + 1;
     const bool lds_walk = d.T <= kMaxLdsFrames;
-    const int K = lds_walk ? max(1, min(W + H, nbw / kSpecMinBlocks)) : 1;
+    const int K = lds_walk ? max(1, min(W + H + XW, nbw / kSpecMinBlocks)) : 1;
 #ifdef WX_PHASE_TIMING
     WX_T(w1);
 #endif
@@ -2780,9 +2794,10 @@ __global__ __launch_bounds__(kWave*(W + H)) __attribute__((amdgpu_waves_per_eu(H
 
 // Split segments: P workgroups (parts, one per CU) per segment, grid = ceil(S / 8) * 8 * P.
 template <int C, int VS, int W>
-__global__ __launch_bounds__(kWave*(W + 2)) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
+__global__ __launch_bounds__(kWave * kSplitWaves) __attribute__((amdgpu_waves_per_eu(1, 2))) void align_dp_split_kernel(
     AlignArgs a) {
-    align_dp_body<C, VS, W, 2, true>(a);
+    static_assert(W + 2 <= kSplitWaves && kSplitWaves <= 8, "split workgroup: W DP waves + 2 helpers + walkers");
+    align_dp_body<C, VS, W, 2, true, kSplitWaves - W - 2>(a);
 }
 
 struct TrellisArgs {

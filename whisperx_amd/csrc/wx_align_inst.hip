@@ -12,7 +12,7 @@ void launch_align_dp(dim3 grid, hipStream_t s, const AlignArgs& a) {
 }
 template <int C, int VS, int W>
 void launch_align_split(dim3 grid, hipStream_t s, const AlignArgs& a) {
-    hipLaunchKernelGGL((align_dp_split_kernel<C, VS, W>), grid, dim3(kWave * (W + 2)), 0, s, a);
+    hipLaunchKernelGGL((align_dp_split_kernel<C, VS, W>), grid, dim3(kWave * kSplitWaves), 0, s, a);
 }
 template <int C, int VS, int W>
 void launch_trellis(dim3 grid, hipStream_t s, const TrellisArgs& a) {
