@@ -194,13 +194,13 @@ def child(args):
                                                              for p_ in range(args.parts)]
                 out[case]["granule_seen_us_by_part_med"] = [[round(float(np.median(rel[:, p_, q, 2])), 2) for q in range(1, nq, 4)]
                                                             for p_ in range(args.parts)]
-            lbuf = (ctypes.c_ulonglong * (n * 16 * 3))()
+            lbuf = (ctypes.c_ulonglong * (n * 32 * 3))()
             lib.wx_debug_loop(lbuf, n)
-            lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 16, 3).astype(np.int64)[perm]
+            lp = np.frombuffer(lbuf, dtype=np.uint64).reshape(n, 32, 3).astype(np.int64)[perm]
             out[case]["loop_med_per_wave"] = [[float(np.median(lp[:, w, i])) for i in range(3)] for w in range(8)
                                               if lp[:, w, 0].max() > 0]
             if args.parts > 1:
-                lq = lp.reshape(-1, args.parts, 16, 3)
+                lq = lp.reshape(-1, args.parts, 32, 3)
                 out[case]["loop_med_by_part"] = [[[float(np.median(lq[:, q, w, i])) for i in range(3)]
                                                   for w in range(8) if lq[:, q, w, 0].max() > 0]
                                                  for q in range(args.parts)]
@@ -214,6 +214,20 @@ def child(args):
             rk = rk[rk[:, 2] > 0]
             if len(rk):
                 out[case]["walk_rl_med(cycles,changes,blocks)"] = [float(np.median(rk[:, i])) for i in range(3)]
+            sw_ = lp[:, 6:13, :]
+            sw_ = sw_[sw_[:, 0, 2] > 0]  # (the workgroups that walked)
+            if len(sw_):  # walk_spec per wave (slots 6 + wave)
+                out[case]["spec_by_wave_med"] = [[float(np.median(sw_[:, w, i])) for i in range(3)]
+                                                 for w in range(7) if sw_[:, w, 1].max() > 0]
+            ww = lp[:, 16:24, :]
+            ww = ww[ww[:, 0, 2] > 0]
+            if len(ww):  # walk_range per wave: window-wait cycles, run-length cycles, blocks
+                out[case]["walk_by_wave_med(win,rl,blocks)"] = [[float(np.median(ww[:, w, i])) for i in range(3)]
+                                                                for w in range(8) if ww[:, w, 2].max() > 0]
+                w2 = lp[:, 24, :]
+                w2 = w2[w2[:, 2] > 0]
+                if len(w2):
+                    out[case]["walk_by_wave_med(win,rl,blocks)"].append([float(np.median(w2[:, i])) for i in range(3)])
             wk = lp[:, 15, :]
             wk = wk[wk[:, 1] > 0]
             if len(wk):
@@ -260,7 +274,7 @@ def main():
                 print(f"            phases {v['phases_cyc_med']} seg_us {v['seg_us_med']:.1f} clk {v['clock_GHz']:.2f} GHz entry_us_q {v['entry_us_q']}", flush=True)
                 for k in ("seg_exit_us_by_N(count,med,max)", "chunk_start_us_by_part_med", "granule_store_us_by_part_med", "granule_seen_us_by_part_med",
                           "fwd_by_part_med", "entry_by_part_med_us", "exit_by_part_med_us", "exit_max_us",
-                          "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_rl_med(cycles,changes,blocks)", "walk_split_med(argmax,walk,compact)",
+                          "loop_med_per_wave", "loop_med_by_part", "handoff_by_part", "walk_rl_med(cycles,changes,blocks)", "walk_split_med(argmax,walk,compact)", "spec_by_wave_med", "walk_by_wave_med(win,rl,blocks)",
                           "handoff_med(misses,wait_cyc,slack_cyc)"):
                     if k in v:
                         print(f"            {k} {v[k]}", flush=True)

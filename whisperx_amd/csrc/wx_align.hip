@@ -1671,7 +1671,7 @@ extern "C" int wx_debug_cq(unsigned long long* host, int n) {
                                     hipMemcpyDeviceToHost);
 }
 extern "C" int wx_debug_loop(unsigned long long* host, int n) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_loop), sizeof(unsigned long long) * 48 * (size_t)n, 0,
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(wx::wx_loop), sizeof(unsigned long long) * wx::kLoopSlots * 3 * (size_t)n, 0,
                                     hipMemcpyDeviceToHost);
 }
 #endif

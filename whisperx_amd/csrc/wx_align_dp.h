@@ -354,7 +354,8 @@ struct Layout {
 // plus s_memrealtime at entry and exit (100 MHz) to convert cycles to time.
 __device__ unsigned long long wx_phase[8192 * 6];
 // per (segment, wave): cycles in steps / barrier waits / other chunk work
-__device__ unsigned long long wx_loop[8192 * 16 * 3];
+constexpr int kLoopSlots = 32;  // per workgroup, 3 counters each
+__device__ unsigned long long wx_loop[8192 * kLoopSlots * 3];
 // per (workgroup, chunk): s_memrealtime when wave 0 passed barrier q, when wave W-1 stored
 // chunk q's halo granules, when wave 0 had chunk q's halo (split kernels)
 __device__ unsigned long long wx_cq[8192 * 48 * 3];
@@ -432,6 +433,7 @@ struct Split {
     // by LDS-DMA, hand-counted vmcnt, its bitmap stores handed to the helper — every missed
     // prefetch cost a round trip inside the chain and the parts drifted apart: 59.7 us.)
     float* xg;  // LDS [2][32]
+    float* q0l;  // LDS [T]: q0 = exp(em[t, 0]), filled by the extra walker waves (nullptr: not kept)
 };
 
 __device__ __forceinline__ void granule_store(uint64_t* g, float v, unsigned tag) {
@@ -633,9 +635,32 @@ struct Forward {
             c0a = __shfl(a, kChunk);
         };
         if (c0prod && nch > 0) c0_make(0, c0_load(0));  // (before barrier 0)
-        if (H && wv >= W + NH) {  // split kernels' extra walker waves: keep the barrier count
+        if (H && wv >= W + NH) {
+            // split kernels' extra walker waves: keep the barrier count, and meanwhile fill
+            // q0 = exp(em[t, 0]) (alignment.py:409's stay probabilities) into this part's LDS for
+            // merge_repeats — the last part to arrive then has it at hand (fill_q0 after the walk
+            // was ~1 us of config 2's tail).  64 rows per wave and chunk, loaded two chunks ahead
+            // (unconditional, clamped), so no barrier waits on a load.
+            float* q0l = SP ? sp->q0l : nullptr;
+            const int nxw = (int)(blockDim.x >> 6) - W - NH;
+            const int step = kWave * nxw;
+            const int l = lane_id();
+            int r0 = (wv - W - NH) * kWave;  // (uniform) first row of this wave's current group
+            float e0 = 0.0f, e1 = 0.0f;
+            if (q0l) {
+                e0 = E[(int64_t)min(r0 + l, T - 1) * V];
+                e1 = E[(int64_t)min(r0 + step + l, T - 1) * V];
+            }
             if (kReg) __syncthreads();  // (barrier -1)
-            for (int q = 0; q < nch; ++q) __syncthreads();
+            for (int q = 0; q < nch; ++q) {  // 64 nxw rows per chunk of 32 rows: done by chunk nch / 2
+                __syncthreads();
+                if (q0l && r0 < T) {
+                    if (r0 + l < T) q0l[r0 + l] = exp_cr(e0);
+                    e0 = e1;
+                    r0 += step;
+                    e1 = E[(int64_t)min(r0 + step + l, T - 1) * V];
+                }
+            }
             return false;
         }
         if (H && wv >= W) {
@@ -911,12 +936,12 @@ struct Forward {
         }
 #ifdef WX_PHASE_TIMING
         if (l == 0 && blockIdx.x < 8192 && MODE != 1) {
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + wv) * 3;
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + wv) * 3;
             o[0] = acc_steps;
             o[1] = acc_bar;
             o[2] = acc_other;
             if (SP && xsub) {  // hand-off: missed prefetches, cycles in the chunk's wait, in slack waits
-                unsigned long long* x = wx_loop + ((size_t)blockIdx.x * 16 + 14) * 3;
+                unsigned long long* x = wx_loop + ((size_t)blockIdx.x * kLoopSlots + 14) * 3;
                 x[0] = x_miss;
                 x[1] = x_wait;
                 x[2] = x_slack;
@@ -1258,7 +1283,7 @@ struct Forward {
         }
 #ifdef WX_PHASE_TIMING
         if (lane_id() == 0 && blockIdx.x < 8192) {  // [work, barrier wait, DMA wait] per helper
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W + (stage ? 0 : 1)) * 3;
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + W + (stage ? 0 : 1)) * 3;
             o[0] = acc_work;
             o[1] = acc_bar;
             o[2] = acc_vm;
@@ -1329,7 +1354,7 @@ struct Forward {
         }
 #ifdef WX_PHASE_TIMING
         if (lane_id() == 0 && blockIdx.x < 8192) {
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + W + (stage ? 0 : 1)) * 3;
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + W + (stage ? 0 : 1)) * 3;
             o[0] = acc_c0;
             o[1] = acc_bar;
             o[2] = acc_other;
@@ -1577,14 +1602,19 @@ __device__ int column_argmax(const float* __restrict__ cn, int T) {
     const int l = lane_id();
     int nan_row = 0x7fffffff, best_row = 0;
     float best = -INFINITY;
-    constexpr int kBatch = 8;  // loads in flight per lane
+    // loads in flight per lane.  WT: the history was written through, so every load goes out
+    // to the fabric (~1 us): one round for T <= 2048 (8 per lane took 3 rounds at T = 1499)
+    constexpr int kBatch = WT ? 32 : 8;
     for (int base = 0; base < T; base += kBatch * kWave) {
         float v[kBatch];
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) {
+        for (int u = 0; u < kBatch; ++u) {  // (unconditional, clamped: no wait at the issue)
             const int i = base + u * kWave + l;
-            v[u] = i < T ? ld_pub<WT>(cn + i) : -INFINITY;
+            v[u] = ld_pub<WT>(cn + min(i, T - 1));
         }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+            if (base + u * kWave + l >= T) v[u] = -INFINITY;
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {  // rows of a lane in increasing order
             const int row = base + u * kWave + l + 1;
@@ -2034,12 +2064,15 @@ struct CkSrc {
 };
 
 struct SpecWalk {
-    int K, L, L0, top;  // segments; blocks per segment (segment 0: L0)
+    int K, L0, Lb, ex, top;  // segments; blocks of segment 0 (L0), of the others (Lb, +1 for k <= ex)
     const int* colrec;  // LDS, per block: the segment walker's column after it (-1: not reached)
     const int* gstart;  // LDS [K]: guessed column at the top of segment k
     const int* sres;    // LDS [K]: the walker's result (-2: the path continues below the segment)
     const int* send;    // LDS [K]: its column after the segment's last block
-    __device__ __forceinline__ int lo(int k) const { return max(top - L0 - k * L + 1, 0); }
+    // segment k covers blocks lo(k) .. lo(k - 1) - 1 (segment 0: up to top); lo(K - 1) = 0
+    __device__ __forceinline__ int lo(int k) const {
+        return k == 0 ? top - L0 + 1 : max(top - L0 - (k * Lb + min(k, ex)) + 1, 0);
+    }
 };
 
 // The backtrack walk (alignment.py:395-421) over the decision bitmap: from column j at the
@@ -2073,13 +2106,20 @@ __device__ __forceinline__ int walk_range(Src& src, int j, int b, unsigned first
     b = uniform(b);
     j = uniform(j);
 #ifdef WX_PHASE_TIMING
-    unsigned long long t_rl = 0, n_ch = 0, n_bl = 0;
+    unsigned long long t_rl = 0, n_ch = 0, n_bl = 0, t_win = 0;
     auto dump = [&]() {
         if (threadIdx.x == 0 && blockIdx.x < 8192) {  // (wave 0's last walk_range)
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + 13) * 3;
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + 13) * 3;
             o[0] = t_rl;
             o[1] = n_ch;
             o[2] = n_bl;
+        }
+        const int wv_ = (int)threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0 && wv_ < 8 && blockIdx.x < 8192) {  // slots 16 + wave (24: wave 0's second walk)
+            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + (spec ? 24 : 16 + wv_)) * 3;
+            o[0] = t_win;  // cycles in the window gather (its load wait)
+            o[1] = t_rl;   // in the run-length loop
+            o[2] = n_bl;   // blocks
         }
     };
 #else
@@ -2104,8 +2144,16 @@ __device__ __forceinline__ int walk_range(Src& src, int j, int b, unsigned first
     auto block = [&](Win& w, Win& wn, Win& wa, int& res) -> bool {
         unsigned win;
         int dd;
+#ifdef WX_PHASE_TIMING
+        WX_T(wi0);
+#endif
         src.window(w, b, j, win, dd);
         win &= first_mask;
+#ifdef WX_PHASE_TIMING
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        WX_T(wi1);
+        t_win += wi1 - wi0;
+#endif
         first_mask = 0xFFFFFFFFu;
         const int d0 = dd;
 #ifdef WX_PHASE_TIMING
@@ -2234,15 +2282,30 @@ __device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn,
     // The segments cover the blocks below T (t_start <= T): the walkers start while wave 0
     // alone finds t_start, so its segment is kSpecArgmaxBlocks shorter than theirs.  (Round 2
     // waited for a workgroup-wide t_start first: 1-2 us slower.)  K == 1: wave 0 walks alone.
+    // Balanced: wave 0 takes its share less the argmax allowance, the other K - 1 segments
+    // split the rest within one block of each other (a uniform length had left the last
+    // walker a single block while the others walked 7 + kSpecOverlap).
     sw.top = (T - 1) >> 5;
-    sw.L = max((sw.top + 1 + kSpecArgmaxBlocks + K - 1) / K, 1);
-    sw.L0 = max(sw.L - kSpecArgmaxBlocks, 1);
-    while (K > 1 && sw.lo(K - 2) == 0) --K;  // (segments past block 0 would be empty)
-    if (K == 1) sw.L0 = sw.top + 1;
+    const int nb = sw.top + 1;
+    sw.L0 = max((nb + kSpecArgmaxBlocks + K / 2) / K - kSpecArgmaxBlocks, 1);
+    if (K > 1 && nb - sw.L0 < K - 1) K = max(nb - sw.L0 + 1, 1);  // (one block per walker at least)
+    if (K <= 1 || sw.L0 >= nb) {
+        K = 1;
+        sw.L0 = nb;
+        sw.Lb = 1;
+        sw.ex = 0;
+    } else {
+        sw.Lb = (nb - sw.L0) / (K - 1);
+        sw.ex = (nb - sw.L0) % (K - 1);
+    }
     sw.K = K;
     sw.sres = sbuf + K;
     sw.send = sbuf + 2 * K;
     const int tref = T;
+#ifdef WX_PHASE_TIMING
+    WX_T(sp0);
+    unsigned long long sp_am = sp0;
+#endif
     // this wave's first walk: wave 0 the top segment from (t_start, N); wave k < K its segment
     // from a guessed column kSpecOverlap blocks above it
     bool go = false;
@@ -2251,6 +2314,9 @@ __device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn,
     int* rec = nullptr;
     if (wv == 0) {
         t_start = column_argmax<Src::kWT>(cn, T);
+#ifdef WX_PHASE_TIMING
+        sp_am = __builtin_amdgcn_s_memtime();
+#endif
         if (t_start <= 0) {
             res = -1;  // (the reference's None)
         } else {
@@ -2287,8 +2353,22 @@ __device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn,
             sbuf[2 * K + wv] = jo;
         }
     }
+#ifdef WX_PHASE_TIMING
+    WX_T(sp1);
+#endif
     wave_fence();
     block_fence();
+#ifdef WX_PHASE_TIMING
+    WX_T(sp2);
+    // per wave (slots 6 + wave): wave 0 [argmax, first walk, barrier] cycles since entry; walkers
+    // [first walk, barrier, K]
+    if (lane == 0 && wv <= 6 && blockIdx.x < 8192) {
+        unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + 6 + wv) * 3;
+        o[0] = wv == 0 ? sp_am - sp0 : sp1 - sp0;
+        o[1] = wv == 0 ? sp1 - sp0 : sp2 - sp0;
+        o[2] = wv == 0 ? sp2 - sp0 : (unsigned long long)K;
+    }
+#endif
     if (wv == 0 && (res == -2 || res == -3)) {
         int j1 = N, b1 = tb;
         unsigned fm1 = fm;
@@ -2330,6 +2410,34 @@ __device__ void compact_starts(const unsigned* cmask, int b_lo, int b_hi, int32_
             const int p = 31 - __clz(mm);
             start[k++] = b * kChunk + (31 - p);
             mm &= ~(1u << p);
+        }
+        base += __shfl(incl, kWave - 1);
+    }
+}
+
+// compact_starts with every wave of the workgroup (every thread calls it): lane b of each
+// 64-block group holds block b's mask and its exclusive popcount prefix; wave w stores the
+// bits at positions 31 - w, 31 - w - nw, ... (token k = prefix + the set bits above the
+// position: frames earlier in the block), so each wave makes 32 / nw conditional stores
+// instead of wave 0 looping over every set bit of a block (1.2 us of config 2's tail).
+__device__ void compact_starts_par(const unsigned* cmask, int b_lo, int b_hi, int32_t* __restrict__ start) {
+    const int lane = lane_id();
+    const int wv = uniform((int)threadIdx.x >> 6), nw = (int)blockDim.x >> 6;
+    int base = 0;
+    for (int b0 = b_lo; b0 <= b_hi; b0 += kWave) {
+        const int b = b0 + lane;
+        const unsigned m = (b <= b_hi) ? cmask[b] : 0u;
+        const int c = __popc(m);
+        int incl = c;
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const int y = __shfl_up(incl, off);
+            if (lane >= off) incl += y;
+        }
+        const int k0 = base + incl - c;
+        for (int p = 31 - wv; p >= 0; p -= nw) {  // bit 31 = lowest frame of the block
+            const unsigned hi = p == 31 ? 0u : m >> (p + 1);
+            if ((m >> p) & 1u) start[k0 + __popc(hi)] = b * kChunk + (31 - p);
         }
         base += __shfl(incl, kWave - 1);
     }
@@ -2578,12 +2686,13 @@ constexpr int kCkSlots =
 
 // Split kernels: waves per workgroup.  Beyond the W DP waves and the two helpers, the rest
 // only keep the forward's barrier count and then walk speculative segments (walk_spec: more
-// walkers, shorter segments).  177 VGPRs allow two waves per SIMD: 8.  (-DWX_SPLIT_WAVES=6:
-// no extra walkers.)
+// walkers, shorter segments).  177 VGPRs allow two waves per SIMD: 8 (12 waves = 168 VGPRs
+// spilled 33 in the register-resident forward).  (-DWX_SPLIT_WAVES=6: no extra walkers.)
 #ifndef WX_SPLIT_WAVES
 #define WX_SPLIT_WAVES 8
 #endif
 constexpr int kSplitWaves = WX_SPLIT_WAVES;
+constexpr int kQ0LdsFrames = 4096;  // Split::q0l rows (longer segments: fill_q0 after the walk)
 
 template <int C, int VS, int W, int H, bool SP = false, int XW = 0>
 __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
@@ -2601,10 +2710,12 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     __shared__ __attribute__((aligned(16))) float xh[W > 1 ? 2 * W * kWave : 1];
     __shared__ unsigned cmask_lds[kMaxLdsFrames / kChunk + 1];
     __shared__ int tsb[3];
+    __shared__ int blo_lds;  // walk_tail: the walk's lowest block (-1: no path)
     __shared__ int colrec_lds[W + H > 1 ? kMaxLdsFrames / kChunk + 1 : 1];  // walk_spec records
     __shared__ int sbuf_lds[3 * (W + H + XW)];
     __shared__ ColMapLds<VS> cml;
     __shared__ float xg_lds[SP && C == 1 ? 2 * 32 : 1];  // Split::xg
+    __shared__ float q0_lds[SP && XW > 0 ? kQ0LdsFrames : 1];  // Split::q0l
     const int P = SP ? a.parts : 1;
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
     // b % 8 — one XCD under the observed round-robin dispatch — and read its emission rows
@@ -2649,6 +2760,7 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         sp.xin = xseg + (part > 0 ? part - 1 : 0) * kHaloCells;
         sp.xout = xseg + part * kHaloCells;
         sp.xg = xg_lds;
+        sp.q0l = (XW > 0 && d.T <= kQ0LdsFrames) ? q0_lds : nullptr;
     }
     if (SP && lane == 0) tsb[2] = 0;
     bool lost = false;
@@ -2710,9 +2822,12 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // wave (walk_spec, which also finds t_start); one wave walks alone
     const int nbw = ((d.T - 1) >> 5) + 1;
     const bool lds_walk = d.T <= kMaxLdsFrames;
+    // q0 already in this workgroup's LDS (Split::q0l; the recovery paths write it to q0)
+    const bool q0l_ok = SP && XW > 0 && d.T <= kQ0LdsFrames && !slow && !failed;
     const int K = lds_walk ? max(1, min(W + H + XW, nbw / kSpecMinBlocks)) : 1;
 #ifdef WX_PHASE_TIMING
     WX_T(w1);
+    unsigned long long wx_w2 = 0;
 #endif
     auto walk_tail = [&](auto& wsrc) {
     int ts = 0, b_lo = -1;
@@ -2729,24 +2844,33 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
         }
 #ifdef WX_PHASE_TIMING
         WX_T(w2);
+        wx_w2 = w2;
 #endif
-        if (b_lo >= 0) {
+        if (!H && b_lo >= 0) {
             wave_fence();
             compact_starts(cmask, b_lo, (ts - 1) >> 5, start);
         }
-        if (lane == 0) tsb[1] = b_lo >= 0 ? 1 : 0;
-#ifdef WX_PHASE_TIMING
-        WX_T(w3);
-        if (lane == 0 && blockIdx.x < 8192) {  // walk-phase split: argmax, walk, compaction
-            unsigned long long* o = wx_loop + ((size_t)blockIdx.x * 16 + 15) * 3;
-            o[0] = w1 - w0;
-            o[1] = w2 - w1;
-            o[2] = w3 - w2;
+        if (lane == 0) {
+            tsb[1] = b_lo >= 0 ? 1 : 0;
+            blo_lds = b_lo;
         }
-#endif
     } else {
-        if (H && !slow && !failed) fill_q0(E, a.V, d.T, q0, kWave);
+        if (H && !slow && !failed && !q0l_ok) fill_q0(E, a.V, d.T, q0, kWave);
     }
+    if constexpr (H != 0) {  // latency / split kernels: the compaction over every wave
+        block_fence();  // (wave 0's change masks, b_lo, t_start)
+        const int bl = uniform(blo_lds);
+        if (bl >= 0) compact_starts_par(cmask, bl, (uniform(tsb[0]) - 1) >> 5, start);
+    }
+#ifdef WX_PHASE_TIMING
+    WX_T(w3);
+    if (lane == 0 && blockIdx.x < 8192) {  // walk-phase split: argmax, walk, compaction
+        unsigned long long* o = wx_loop + ((size_t)blockIdx.x * kLoopSlots + 15) * 3;
+        o[0] = w1 - w0;
+        o[1] = wx_w2 - w1;
+        o[2] = w3 - wx_w2;
+    }
+#endif
     };
     if constexpr (CK) {
         CkSrc<C, VS> wsrc;
@@ -2779,9 +2903,11 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if (!ok) return;
     // (staging costs one more round trip: it pays when every thread has several tokens)
     if (d.T + d.N <= kLdsFloats && d.N > 2 * (int)blockDim.x)
-        merge_tokens_lds(E, a.V, a.tok + d.tok0, d.N, d.T, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0, lds);
+        merge_tokens_lds(E, a.V, a.tok + d.tok0, d.N, d.T, ts, q0l_ok ? q0_lds : q0, start, a.seg_end + d.tok0,
+                         a.seg_score + d.tok0, lds);
     else
-        merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0, start, a.seg_end + d.tok0, a.seg_score + d.tok0);
+        merge_tokens(E, a.V, a.tok + d.tok0, d.N, ts, q0l_ok ? q0_lds : q0, start, a.seg_end + d.tok0,
+                     a.seg_score + d.tok0);
     WX_STAMP(3);
     WX_STAMP_RT(5);
 }
