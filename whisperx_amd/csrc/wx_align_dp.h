@@ -2069,6 +2069,12 @@ struct SpecWalk {
     const int* gstart;  // LDS [K]: guessed column at the top of segment k
     const int* sres;    // LDS [K]: the walker's result (-2: the path continues below the segment)
     const int* send;    // LDS [K]: its column after the segment's last block
+    // after the barrier: gstart / sres / send of segment `lane` in lane `lane` (read by
+    // v_readlane: the merge chain was a serial LDS round trip per segment)
+    int vg, vr, ve;
+    __device__ __forceinline__ int gst(int k) const { return __builtin_amdgcn_readlane(vg, k); }
+    __device__ __forceinline__ int res(int k) const { return __builtin_amdgcn_readlane(vr, k); }
+    __device__ __forceinline__ int end(int k) const { return __builtin_amdgcn_readlane(ve, k); }
     // segment k covers blocks lo(k) .. lo(k - 1) - 1 (segment 0: up to top); lo(K - 1) = 0
     __device__ __forceinline__ int lo(int k) const {
         return k == 0 ? top - L0 + 1 : max(top - L0 - (k * Lb + min(k, ex)) + 1, 0);
@@ -2187,12 +2193,12 @@ __device__ __forceinline__ int walk_range(Src& src, int j, int b, unsigned first
             bool merged = k >= 1 && bb != spec->lo(k) && jj == uniform(((const lds_int*)spec->colrec)[bb]);
             for (;;) {
                 if (merged) {
-                    r = uniform(((const lds_int*)spec->sres)[k]);
+                    r = spec->res(k);
                     bb = spec->lo(k);
-                    jj = uniform(((const lds_int*)spec->send)[k]);
+                    jj = spec->end(k);
                     if (r != -2) break;
                 }
-                merged = bb == spec->lo(k) && k + 1 < spec->K && jj == uniform(((const lds_int*)spec->gstart)[k + 1]);
+                merged = bb == spec->lo(k) && k + 1 < spec->K && jj == spec->gst(k + 1);
                 if (!merged) break;
                 ++k;
             }
@@ -2372,12 +2378,16 @@ __device__ __forceinline__ int walk_spec(Src& lw, int N, int T, const float* cn,
     if (wv == 0 && (res == -2 || res == -3)) {
         int j1 = N, b1 = tb;
         unsigned fm1 = fm;
+        const int kl = min(lane, K - 1);  // (K <= waves <= 64)
+        sw.vg = sbuf[kl];
+        sw.vr = sbuf[K + kl];
+        sw.ve = sbuf[2 * K + kl];
         if (res == -2) {
             // segments entered on their guessed column are the true walk's as a whole
             int k = 1;
-            for (; k < K && jo == uniform(sbuf[k]); ++k) {
-                res = uniform(sbuf[K + k]);
-                jo = uniform(sbuf[2 * K + k]);
+            for (; k < K && jo == sw.gst(k); ++k) {
+                res = sw.res(k);
+                jo = sw.end(k);
                 if (res != -2) return res;
             }
             j1 = jo;
