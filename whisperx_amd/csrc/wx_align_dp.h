@@ -1056,6 +1056,7 @@ struct Forward {
         const int l = lane_id();
         const int rr = l & 31;
         const float e = buf[(rr >> 2) * kQS + (rr & 3)];  // column 0 of row rr
+#ifdef WX_COL0_DPP
         float x = l >= 32 ? e : 0.0f;
         double a = acc;
 #pragma unroll
@@ -1064,6 +1065,44 @@ struct Forward {
             x = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x130 /* wave_shl:1 */,
                                                                    0xF, 0xF, true));
         }
+#else
+        // Round 5: the same sums with the row values uniform.  Lane j converts em[t0 + j, 0]
+        // (one instruction for the chunk), the doubles go through LDS and come back broadcast
+        // (16-byte reads, every lane the same address), and at step j the lanes r > j add row
+        // j: an EXEC-masked v_add_f64 with a scalar s_bitset0 retiring lane j + 1 after it.  Lane
+        // r thus adds em[t0 + 0 .. r - 1, 0] in row order onto S(t0) and nothing else — the
+        // sequential chain's additions exactly, no +0 terms.  Two instructions per row instead
+        // of a conversion, a DPP shift and the add (the column-0 helper paced part 0: with half
+        // rows — a timing experiment with wrong results — config 2 ran 50.8 -> 46.1 us; this form:
+        // 50.8 -> 47.5 us, bit-identical).  -DWX_COL0_DPP builds the previous form.
+        __shared__ __attribute__((aligned(16))) double c0d[kChunk];
+        if (l < kChunk) c0d[l] = (double)e;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (other lanes' writes, read below)
+        double dv[kChunk];
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) dv[j] = c0d[j];
+        double a = acc;
+        unsigned long long sv;
+#define WX_C0_STEP(J, BIT) "v_add_f64 %[a], %[a], %[d" #J "]\n\ts_bitset0_b64 exec, " #BIT "\n\t"
+#define WX_C0_BLOCK(B, J0, B1, B2, B3, B4, B5, B6, B7, B8)                                                      \
+        asm volatile("s_mov_b64 %[sv], exec\n\t"                                                              \
+                     "s_mov_b32 exec_lo, %[mlo]\n\t"                                                          \
+                     "s_mov_b32 exec_hi, 1\n\t" WX_C0_STEP(0, B1) WX_C0_STEP(1, B2) WX_C0_STEP(2, B3)          \
+                         WX_C0_STEP(3, B4) WX_C0_STEP(4, B5) WX_C0_STEP(5, B6) WX_C0_STEP(6, B7)               \
+                             WX_C0_STEP(7, B8) "s_mov_b64 exec, %[sv]\n\t"                                    \
+                     : [a] "+v"(a), [sv] "=&s"(sv)                                                             \
+                     : [mlo] "s"((unsigned)(0xFFFFFFFFu << ((J0) + 1))), [d0] "v"(dv[(J0)]),                  \
+                       [d1] "v"(dv[(J0) + 1]), [d2] "v"(dv[(J0) + 2]), [d3] "v"(dv[(J0) + 3]),                 \
+                       [d4] "v"(dv[(J0) + 4]), [d5] "v"(dv[(J0) + 5]), [d6] "v"(dv[(J0) + 6]),                 \
+                       [d7] "v"(dv[(J0) + 7]))
+        // block b: rows 8b .. 8b + 7, lanes 8b + 1 .. 32 active at its start (exec_hi = lane 32)
+        WX_C0_BLOCK(0, 0, 1, 2, 3, 4, 5, 6, 7, 8);
+        WX_C0_BLOCK(1, 8, 9, 10, 11, 12, 13, 14, 15, 16);
+        WX_C0_BLOCK(2, 16, 17, 18, 19, 20, 21, 22, 23, 24);
+        WX_C0_BLOCK(3, 24, 25, 26, 27, 28, 29, 30, 31, 32);
+#undef WX_C0_BLOCK
+#undef WX_C0_STEP
+#endif
         acc = __shfl(a, 32);  // S(t0 + 32): the next chunk's start (uniform)
         if (l < 32) {
             const int t = q * kChunk + l;
