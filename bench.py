@@ -70,7 +70,7 @@ def pmc_traffic(kernel):
     (profiles/r*_pmc_traffic.json: separate FETCH_SIZE / WRITE_SIZE passes over this same
     command, gfx950 FETCH_SIZE correction applied) — or None when none matches."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r*_pmc_traffic*.json")))
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
@@ -201,8 +201,9 @@ def e2e_align(device, n_seg=16, seed=7):
     n_words = len(out["word_segments"])
     return {"value": 30.0 * n_seg / dt, "unit": "audio-sec/s", "segments": n_seg, "words": n_words,
             "ms_per_segment": 1000 * dt / n_seg, "dp": _recovered_since(st0),
-            "note": "align() incl. random-weight wav2vec2-base fp32 forward per segment on the GPU "
-                    "(8 HIP streams, one unpadded forward per segment)"}
+            "note": "align() incl. random-weight wav2vec2-base fp32 forward on the GPU: the packed encoder "
+                    "(segments stacked by rows through one transformer pass, per-segment attention and "
+                    "positional conv), fused DP, host aggregation overlapped with the forwards"}
 
 
 def e2e_config3(device, seed=3):
@@ -574,6 +575,88 @@ def mae_e2e(device, n_seg=4, seed=7, large=False, seg_s=30.0):
             "vs": "reference CPU align() path (CPU forward + CPU DP), same weights and audio"}
 
 
+def config5_leg(device, n_seg=8, seed=5, cpu_budget_s=20.0, dp_steps=20):
+    """BASELINE config 5: German wav2vec2-large-xlsr-shaped model (24 x 1024, layer-norm feature
+    encoder, stable layer norm; random weights), V = 40, long-form 60 s segments (T = 2999).
+    (a) align() end to end on the GPU over n_seg x 60 s: audio-s/s and ms per segment;
+    (b) the fused DP alone on 64 x T=2999, V=40, N~U[850,950] with emissions resident in HBM:
+        device time of back-to-back launches, algorithmic bytes, HBM fraction, and the PMC
+        traffic of the committed rocprofv3 summary for the same kernel;
+    (c) the reference-structured CPU align() (CPU forward + TorchPort DP + host aggregation) on
+        one 60 s clip at every usable host thread, repeated for ~cpu_budget_s."""
+    import whisperx_amd
+    from whisperx_amd import _lib, synthetic
+
+    out = {}
+    model = _w2v_large(device, seed)
+    dictionary, letters = synthetic.de_dictionary(), synthetic.DE_LETTERS
+    meta = {"language": "de", "dictionary": dictionary, "type": "huggingface"}
+    tr = synthetic.Transcriber(seed, letters=letters)
+    segs = tr.segments([{"start": 60.0 * k, "end": 60.0 * (k + 1)} for k in range(n_seg)])
+    g = torch.Generator().manual_seed(seed)
+    audio = torch.randn(int(60 * n_seg * 16000), generator=g) * 0.1
+    whisperx_amd.align([dict(x) for x in segs[:2]], model, meta, audio, device)  # warm-up
+    torch.cuda.synchronize()
+    st0 = _dp_stats()
+    t0 = time.perf_counter()
+    res = whisperx_amd.align([dict(x) for x in segs], model, meta, audio, device)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out["align"] = {"value": 60.0 * n_seg / dt, "unit": "audio-sec/s", "segments": n_seg, "segment_s": 60.0,
+                    "ms_per_segment": 1000 * dt / n_seg, "words": len(res["word_segments"]),
+                    "dp": _recovered_since(st0)}
+    del model
+    torch.cuda.empty_cache()
+    # (b) DP only
+    rng = np.random.default_rng(55)
+    ems, toks = make_batch(rng, 64, 2999, 40, 850, 950, device)
+    b = _lib.Batch(ems, toks, [0] * len(ems), device=device)
+    del ems
+    plan = _lib.AlignPlan(b)
+    _h, d = time_steps(plan, dp_steps, 3, False)
+    launch_s = d / dp_steps
+    B = algorithmic_bytes(b.Ts, b.Ns, 40)
+    knames = _lib.align_dp_plan(b.S, b.min_N, b.max_N, 40)
+    traffic, src = pmc_traffic(knames[0]) if knames else (None, None)
+    out["dp_only"] = {"segments": b.S, "T": 2999, "V": 40, "N": [850, 950], "kernel": ";".join(knames),
+                      "us_per_launch": launch_s * 1e6, "audio_sec_per_s": sum(b.Ts) * FRAME_S / launch_s,
+                      "bytes_per_launch": B, "achieved_GBps": B / launch_s / 1e9,
+                      "frac": B / launch_s / 1e9 / HBM_PEAK_GBPS, "traffic": traffic,
+                      "traffic_ratio": (traffic / B) if traffic else None, "traffic_source": src,
+                      "us_per_launch_events": time_steps.last_launch_s * 1e6,
+                      "dp": _lib.status_summary(plan.status[: b.S])}
+    del plan, b
+    torch.cuda.empty_cache()
+    # (c) CPU align() of the same shape
+    thr = _host_threads()
+    old = torch.get_num_threads()
+    torch.set_num_threads(thr)
+    try:
+        mc = _w2v_large("cpu", seed)
+        one = segs[:1]
+        wav = audio[None, : 60 * 16000]
+        _cpu_reference_align(one, mc, dictionary, wav, lang="de")  # warm-up
+        n, tot = 0, [0.0, 0.0, 0.0]
+        while sum(tot) < cpu_budget_s and n < 20:
+            _, ph = _cpu_reference_align(one, mc, dictionary, wav, lang="de")
+            tot = [a + c for a, c in zip(tot, ph)]
+            n += 1
+            log(f"bench: cfg5 cpu align clip {n}: {sum(ph):.2f} s")
+        el = sum(tot)
+        out["cpu_align"] = {"value": 60.0 * n / el, "unit": "audio-sec/s", "threads": thr, "clips": n,
+                            "ms_per_clip": 1000 * el / n, "forward_ms": 1000 * tot[0] / n, "dp_ms": 1000 * tot[1] / n,
+                            "aggregate_ms": 1000 * tot[2] / n, "cpu_model": _cpu_model(), "kind": "port",
+                            "sample": "one 60 s DE clip (T=2999), random-weight large-xlsr shape, CPU forward + "
+                                      "TorchPort DP + host aggregation"}
+        del mc
+    finally:
+        torch.set_num_threads(old)
+    out["gpu_over_cpu"] = out["align"]["value"] / out["cpu_align"]["value"]
+    out["note"] = ("BASELINE configs[4] on one GPU (the 8-GPU curve is the driver's SCALE run); random weights, "
+                   "synthetic audio and transcripts: timings only (parity: mae_e2e_cfg5)")
+    return out
+
+
 def _recovered_since(before):
     """Segments the legs' align() calls recomputed in-kernel after a lost split hand-off
     (WX_STATUS_RECOVERED), since `before` (a copy of alignment.DP_STATS)."""
@@ -619,7 +702,9 @@ def host_share_leg(k):
     rate = shard_audio / res["wall_s"]
     pred_wall = max(loads) / rate
     print(json.dumps({"ranks_modelled": k, "rank": 0, "cpus": len(pin["cpus"] or []), "threads": pin["threads"],
-                      "numa_node": pin["numa"], "shard_audio_sec": shard_audio, "files": res["files"],
+                      "cpu_set": _cpu_ranges(pin["cpus"]), "numa_node": pin["numa"],
+                      "numa_source": pin["numa_source"], "numa_reason": pin["numa_reason"],
+                      "shard_audio_sec": shard_audio, "files": res["files"],
                       "segments": res["segments"], "wall_s": res["wall_s"], "audio_sec_per_s": rate,
                       "predicted_node_audio_sec_per_s": float(sum(durs)) / pred_wall,
                       "predicted_node_wall_s": pred_wall,
@@ -699,6 +784,13 @@ def main():
         else:
             torch.distributed.init_process_group(backend)
     _allreduce.dev = device if backend == "nccl" else torch.device("cpu")
+    ranks = None
+    if dist_on:  # every rank's host share and device, for the driver's SCALE line (rank 0 prints)
+        ranks = [None] * world
+        torch.distributed.all_gather_object(ranks, {
+            "rank": rank, "local_rank": local_rank, "device": gpu, "numa": pin["numa"],
+            "numa_source": pin["numa_source"], "numa_reason": pin["numa_reason"], "threads": pin["threads"],
+            "cpus": _cpu_ranges(pin["cpus"])})
 
     from whisperx_amd import _lib
     from whisperx_amd.distributed import broadcast_dictionary
@@ -731,7 +823,9 @@ def main():
     out = None
     if rank == 0:
         B = algorithmic_bytes(batch.Ts, batch.Ns, V)
-        launch_s = time_steps.last_launch_s  # HIP events around each step's kernel
+        # the kernel's time per launch: the device time of the K back-to-back timed launches (one
+        # launch per step), not the per-launch event pairs, whose bracketing adds its own gaps
+        launch_s = dev_s / args.steps
         achieved = B / launch_s / 1e9
         knames = _lib.align_dp_plan(batch.S, batch.min_N, batch.max_N, V)  # kernels this step launches
         kname = knames[0] if knames else "?"
@@ -759,7 +853,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname + (" (the step's only launch)" if len(knames) == 1 else
                                             f" (+{len(knames) - 1} more launches)"),
-                         "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6},
+                         "bytes_per_launch": B, "avg_launch_us": launch_s * 1e6,
+                         "avg_launch_us_source": "device time of the timed back-to-back launches / steps",
+                         "avg_launch_us_events": time_steps.last_launch_s * 1e6,
+                         "traffic_ratio": (traffic / B) if traffic else None},
         }
         out["roofline"]["dp"] = _lib.status_summary(plan.status[: batch.S])
         # The latency roofline: a segment's T steps are a dependent chain, and one step of the
@@ -775,6 +872,9 @@ def main():
         out["mae_ms"] = mae
         out["mae_detail"] = {"tokens": ntok, "segments_with_path_mismatch": nbad, "vs": "CPU oracle, same emission"}
         extra = {}
+        if ranks is not None:
+            extra["ranks"] = {"world_size": world, "backend": "rccl" if backend == "nccl" else backend,
+                              "per_rank": ranks}
         if corpus is not None:
             extra["config4_10h_corpus"] = corpus
         if not args.no_corpus:
@@ -817,7 +917,12 @@ def main():
             h3, d3 = time_steps(p3, 3, 1, False)
             B3 = algorithmic_bytes(b3.Ts, b3.Ns, V)
             log("bench: saturated T=3000 done")
+            k3 = _lib.align_dp_plan(b3.S, b3.min_N, b3.max_N, V)
+            t3, t3src = pmc_traffic(k3[0]) if k3 else (None, None)
             extra["saturated_T3000"] = {"segments": n3, "ms_per_step": 1000 * d3 / 3,
+                                        "kernel": ";".join(k3), "bytes_per_launch": B3,
+                                        "traffic": t3, "traffic_ratio": (t3 / B3) if t3 else None,
+                                        "traffic_source": t3src,
                                         "audio_sec_per_s": sum(b3.Ts) * FRAME_S / (d3 / 3),
                                         "achieved_GBps": B3 / (d3 / 3) / 1e9,
                                         "frac": B3 / (d3 / 3) / 1e9 / HBM_PEAK_GBPS,
@@ -901,6 +1006,11 @@ def main():
                 extra["mae_e2e"] = me
             except Exception as e:
                 extra["mae_e2e"] = {"error": repr(e)[:300]}
+            log("bench: config 5 ...")
+            try:
+                extra["config5"] = config5_leg(device)
+            except Exception as e:  # never let the secondary leg hide the primary line
+                extra["config5"] = {"error": repr(e)[:300]}
             try:  # config 5: the layer-norm (large-xlsr) family, V = 40, 60 s segments
                 m5 = mae_e2e(device, n_seg=2, seed=5, large=True, seg_s=60.0)
                 out["mae_e2e_cfg5_ms"] = m5["mae_ms"]
@@ -927,6 +1037,20 @@ def _host_threads():
     from whisperx_amd.distributed import thread_budget
 
     return thread_budget()
+
+
+def _cpu_ranges(cpus):
+    """[0, 1, 2, 5] -> "0-2,5" (None stays None)."""
+    if cpus is None:
+        return None
+    cpus, out, i = sorted(cpus), [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(f"{cpus[i]}-{cpus[j]}" if j > i else f"{cpus[i]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def _cpu_model():

@@ -80,6 +80,13 @@ int wx_trellis(const float* em, const int64_t* em_off, int32_t V,
                const int32_t* tok, const int64_t* tok_off, const int32_t* blank_id,
                int32_t S, int64_t max_N, float* trellis, const int64_t* tr_off, void* stream);
 
+/* Column 0 of get_trellis (alignment.py:367, `torch.cumsum(emission[:, 0], 0)`): the running
+ * sums S(t) = em[0,0] + ... + em[t-1,0] for t = 0..T, accumulated in double in row order as
+ * torch's CPU cumsum does, written to S[0..T] (fp64; the trellis holds them rounded to fp32).
+ * em is a [T, V] fp32 row-major matrix on the device.  The fused DP's column-0 routine, one
+ * wave (it exists to pin that routine bit for bit against the sequential sum). */
+int wx_column0_cumsum(const float* em, int64_t T, int32_t V, double* S, void* stream);
+
 /* backtrack (alignment.py:387-421) from a materialised trellis, batched.  The path of
  * segment s is written in forward (time-increasing) order at element em_off[s] of
  * path_tok/path_time/path_prob (capacity T_s); path_len[s] = its length or -1 (None);

@@ -68,30 +68,79 @@ def test_rank_cpus_numa_split_and_fallback():
     assert rank_cpus_numa(aff, 3, 8, {"gpu_nodes": [0, 1], "node_cpus": topo["node_cpus"]}) == rank_cpus(aff, 3, 8)
 
 
-def test_host_topology_from_fake_sysfs(tmp_path, monkeypatch):
-    """KFD nodes (CPU agents skipped), PCI location -> numa_node, node cpulists, visibility."""
-    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        monkeypatch.delenv(v, raising=False)
-    base = tmp_path / "class/kfd/kfd/topology/nodes"
-    gpus = [(0x0c, 1), (0x8c, 0), (0x1c, 1)]  # (bus, numa) of three GPUs in KFD order
+def _fake_sysfs(root, gpus, node_cpulists):
+    """A KFD topology under `root`: one CPU agent, then GPUs [(pci bus, numa node)] in KFD order;
+    node cpulists {node: "a-b,c"}."""
+    base = root / "class/kfd/kfd/topology/nodes"
     (base / "0").mkdir(parents=True)
     (base / "0" / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
     for i, (bus, node) in enumerate(gpus, start=1):
         (base / str(i)).mkdir()
         (base / str(i) / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
-        dev = tmp_path / f"bus/pci/devices/0000:{bus:02x}:00.0"
+        dev = root / f"bus/pci/devices/0000:{bus:02x}:00.0"
         dev.mkdir(parents=True)
         (dev / "numa_node").write_text(f"{node}\n")
-    for node, cl in ((0, "0-3,8-11"), (1, "4-7,12-15")):
-        d = tmp_path / f"devices/system/node/node{node}"
+    for node, cl in node_cpulists.items():
+        d = root / f"devices/system/node/node{node}"
         d.mkdir(parents=True)
         (d / "cpulist").write_text(cl + "\n")
-    topo = host_topology(str(tmp_path))
+    return str(root)
+
+
+def test_host_topology_from_fake_sysfs(tmp_path, monkeypatch):
+    """KFD nodes (CPU agents skipped), PCI location -> numa_node, node cpulists, visibility:
+    ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES, or CUDA_VISIBLE_DEVICES only when HIP_ is
+    unset; an unmappable entry (UUID, out of range) gives no topology rather than a wrong one."""
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    root = _fake_sysfs(tmp_path, [(0x0c, 1), (0x8c, 0), (0x1c, 1)], {0: "0-3,8-11", 1: "4-7,12-15"})
+    topo = host_topology(root)
     assert topo["gpu_nodes"] == [1, 0, 1]
     assert topo["node_cpus"] == {0: [0, 1, 2, 3, 8, 9, 10, 11], 1: [4, 5, 6, 7, 12, 13, 14, 15]}
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,1")
-    assert host_topology(str(tmp_path))["gpu_nodes"] == [1, 0]
+    assert host_topology(root)["gpu_nodes"] == [1, 0]
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "0")  # ignored while HIP_VISIBLE_DEVICES is set
+    assert host_topology(root)["gpu_nodes"] == [1, 0]
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert host_topology(root)["gpu_nodes"] == [1]
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1,2")  # applied first: CUDA's 0 -> KFD GPU 1
+    assert host_topology(root)["gpu_nodes"] == [0]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-5f1c2a3b")  # UUID: no reliable map
+    assert host_topology(root) is None
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "7")  # out of range
+    assert host_topology(root) is None
+    assert host_topology(root, visible_only=False)["gpu_nodes"] == [1, 0, 1]
     assert host_topology(str(tmp_path / "missing")) is None
+
+
+def test_pin_rank_node_model_with_fewer_visible_gpus(tmp_path, monkeypatch):
+    """One visible GPU modelling rank r of an 8-GPU node: the KFD's full GPU list stands in
+    (numa_source "node_model"), and the reason is recorded when nothing can be modelled."""
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    aff = sorted(os.sched_getaffinity(0))
+    if len(aff) < 2:
+        pytest.skip("needs two CPUs")
+    half = len(aff) // 2
+    cl = {0: ",".join(map(str, aff[:half])), 1: ",".join(map(str, aff[half:]))}
+    root = _fake_sysfs(tmp_path / "n8", [(0x10 + 0x10 * i, i // 4) for i in range(8)], cl)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    old = os.sched_getaffinity(0)
+    try:
+        for r in (0, 5):
+            pin = pin_rank(r, 8, sysfs=root)
+            os.sched_setaffinity(0, old)
+            assert pin["numa_source"] == "node_model" and pin["numa"] == r // 4, pin
+            assert set(pin["cpus"]) <= set(aff[:half] if r < 4 else aff[half:])
+        pin = pin_rank(0, 8, sysfs=str(tmp_path / "missing"))
+        os.sched_setaffinity(0, old)
+        assert pin["numa"] is None and pin["numa_source"] is None and "KFD" in pin["numa_reason"], pin
+        root2 = _fake_sysfs(tmp_path / "n2", [(0x10, 0), (0x20, 1)], cl)
+        pin = pin_rank(0, 8, sysfs=root2)
+        os.sched_setaffinity(0, old)
+        assert pin["numa"] is None and "2 GPU(s)" in pin["numa_reason"], pin
+    finally:
+        os.sched_setaffinity(0, old)
 
 
 def test_lpt_plan_config4():
@@ -119,11 +168,15 @@ def _fake_numa(world):
     return {"gpu_nodes": [1 - r % 2 for r in range(world)], "node_cpus": {0: cpus[:half], 1: cpus[half:]}}
 
 
-def _worker(rank, world, port, q, numa=False):
+def _worker(rank, world, port, q, numa=False, sysfs=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     # before anything else, as bench.py's ranks do
-    pin = pin_rank(rank, world, topology=_fake_numa(world) if numa else "auto")
+    if sysfs:  # fewer visible GPUs than ranks: the node model
+        os.environ["HIP_VISIBLE_DEVICES"] = "0"
+        pin = pin_rank(rank, world, sysfs=sysfs)
+    else:
+        pin = pin_rank(rank, world, topology=_fake_numa(world) if numa else "auto")
     pin["affinity"] = sorted(os.sched_getaffinity(0))
     pin["torch_threads"] = torch.get_num_threads()
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -137,12 +190,18 @@ def _worker(rank, world, port, q, numa=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("numa", [False, True], ids=["host", "fake_numa"])
-def test_gloo_world2_broadcast_and_gather(numa):
+@pytest.mark.parametrize("numa", [False, True, "node_model"], ids=["host", "fake_numa", "fewer_visible_gpus"])
+def test_gloo_world2_broadcast_and_gather(numa, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, numa)) for r in range(2)]
+    sysfs = None
+    if numa == "node_model":  # a 2-GPU node whose ranks each see one GPU: GPU r on node 1 - r
+        cpus = sorted(os.sched_getaffinity(0))
+        half = len(cpus) // 2
+        sysfs = _fake_sysfs(tmp_path, [(0x10, 1), (0x20, 0)],
+                            {0: ",".join(map(str, cpus[:half])), 1: ",".join(map(str, cpus[half:]))})
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, numa is True, sysfs)) for r in range(2)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in procs]
@@ -166,6 +225,7 @@ def test_gloo_world2_broadcast_and_gather(numa):
         for r, o in enumerate(outs):
             assert set(o[3]["cpus"]) <= set(topo["node_cpus"][topo["gpu_nodes"][r]])
             assert o[3]["numa"] == topo["gpu_nodes"][r]
+            assert o[3]["numa_source"] == ("node_model" if numa == "node_model" else "given")
     merged = outs[0][2]
     assert outs[1][2] is None
     assert sorted(merged) == [0, 1, 2, 3, 4]

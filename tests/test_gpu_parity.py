@@ -369,6 +369,109 @@ def test_align_dp_lost_handoff_recovered(monkeypatch):
     assert int(((sts[0] & _lib.STATUS_RECOVERED) != 0).sum()) == 0, sts[0]
 
 
+def _column0_variants(rng, T):
+    """Columns 0 that exercise every branch of the fused DP's column-0 routine (col0_scan's
+    binade scan, its one-row sequential steps, the sequential-chain fallback): log-probs,
+    tiny values, mixed signs, 2^-4-quantised values (exact ties), magnitudes over 2^-40..2^40,
+    -inf rows, a NaN row, +inf after -inf (NaN sums)."""
+    out = {}
+    lg = rng.standard_normal((T, 32)).astype(np.float32)
+    lg[:, 0] += 6.0
+    out["logprob"] = torch.log_softmax(torch.from_numpy(lg), -1).numpy()[:, 0]
+    out["tiny"] = (-rng.random(T) * 1e-7).astype(np.float32)
+    out["mixed"] = (rng.standard_normal(T) * 3).astype(np.float32)
+    out["ties"] = (np.round(rng.standard_normal(T) * 16) / 16).astype(np.float32)
+    out["wide"] = (-np.exp(rng.standard_normal(T) * 9)).astype(np.float32)
+    out["alt_pow2"] = (np.where(np.arange(T) % 2, 1.0, -1.0) * 2.0 ** rng.integers(-20, 20, T)).astype(np.float32)
+    x = (-rng.random(T)).astype(np.float32)
+    x[T // 3] = -np.inf
+    out["neg_inf"] = x.copy()
+    x[2 * T // 3] = np.inf
+    out["inf_nan"] = x.copy()
+    y = (-rng.random(T)).astype(np.float32)
+    y[T // 2] = np.nan
+    out["nan"] = y
+    return out
+
+
+def test_column0_cumsum_bit_exact():
+    """wx_column0_cumsum (the fused DP's column-0 routine) equals the sequential fp64 running
+    sum of em[:, 0] (alignment.py:367, torch's CPU cumsum accumulates in double) bit for bit,
+    NaN for NaN, on every variant and at chunk edges."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(31)
+    for T in (0, 1, 2, 31, 32, 33, 64, 65, 1499, 3001):
+        for name, col in _column0_variants(rng, max(T, 1)).items():
+            col = col[:T]
+            em = np.zeros((T, 3), np.float32)
+            em[:, 0] = col
+            got = _lib.column0_cumsum(torch.from_numpy(em).to(DEV)).cpu().numpy()
+            want = np.concatenate([[0.0], np.cumsum(col.astype(np.float64))])  # sequential (np accumulate)
+            same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+            assert same.all(), f"T={T} {name}: first difference at t={int(np.argmin(same))}"
+
+
+def test_align_dp_column0_edge_values_vs_oracle():
+    """The split kernels' column 0 (col0_pre via col0_chunk) on the column-0 variants above,
+    config-2-sized segments, in the auto (split) and every explicit split shape."""
+    rng = np.random.default_rng(32)
+    cases = []
+    for name, col in _column0_variants(rng, 1499).items():
+        c = _random_cases(rng, 1, (1499, 1500), (300, 500), 32, blank=3)[0]
+        c["em"] = c["em"].copy()
+        c["em"][:, 0] = col
+        cases.append(c)
+    for mode in (-1, 12, 13, 14):
+        _check_vs_oracle(cases, f"column-0 variants mode {mode}", mode)
+
+
+def test_align_dp_split_arrival_fenced_equals_write_through_across_xcds(monkeypatch):
+    """The split kernels hand their decision words and column-N history to the last part with
+    write-through (sc1) stores and loads and no fences (measured behaviour on gfx950, not an
+    architectural guarantee).  With each segment's parts forced onto different XCDs
+    (WX_SPLIT_XCD_SPREAD=1), the fence-free and the fenced arrival (WX_SPLIT_FENCED=1: the
+    memory model's release / acquire on top) give bit-identical results equal to the oracle,
+    in every split shape and on the lost-hand-off recovery path (WX_SPIN_LIMIT=0)."""
+    from whisperx_amd import _lib
+
+    rng = np.random.default_rng(41)
+    cases = _random_cases(rng, 20, (1400, 1500), (300, 500), 32, blank=0)
+    cases += _random_cases(rng, 2, (2900, 3000), (850, 950), 32)
+    cases += _random_cases(rng, 2, (300, 900), (100, 280), 32, quant=16)
+    cases += _random_cases(rng, 2, (5, 40), (20, 60), 32)  # N > T
+    b = _batch(cases)
+    for spin in (None, "0"):
+        if spin is None:
+            monkeypatch.delenv("WX_SPIN_LIMIT", raising=False)
+        else:
+            monkeypatch.setenv("WX_SPIN_LIMIT", spin)
+        for mode in (-1, 12, 13, 14):
+            ref = None
+            for fenced in ("0", "1"):
+                for spread in ("0", "1"):
+                    monkeypatch.setenv("WX_SPLIT_FENCED", fenced)
+                    monkeypatch.setenv("WX_SPLIT_XCD_SPREAD", spread)
+                    tag = f"spin {spin} mode {mode} fenced {fenced} spread {spread}"
+                    ss, se, sc, ts, st = (x.cpu().numpy() for x in _lib.align_dp(b, mode=mode))
+                    # per segment: t_start, outcome and, where a path exists, its spans and scores
+                    # (a failed segment's token slots are not written)
+                    out = []
+                    for s in range(b.S):
+                        a, e = b.tok_off[s], b.tok_off[s + 1]
+                        ok = bool(_lib.status_ok(st[s]))
+                        out.append((int(ts[s]), int(st[s]) & _lib.STATUS_MASK,
+                                    (ss[a:e].tobytes(), se[a:e].tobytes(), sc[a:e].tobytes()) if ok else None))
+                    if ref is None:
+                        ref = out
+                        _check_vs_oracle(cases, tag, mode)
+                    else:
+                        diff = [s for s in range(b.S) if out[s] != ref[s]]
+                        assert not diff, f"{tag}: segments {diff} differ from the unfenced same-XCD launch"
+    monkeypatch.delenv("WX_SPLIT_FENCED")
+    monkeypatch.delenv("WX_SPLIT_XCD_SPREAD")
+
+
 def test_align_dp_handoff_region_reuse():
     """wx_align_dp_ex: one caller-owned hand-off region reused across launches of different
     batch layouts (granules of earlier launches stay behind in other slots: their epochs

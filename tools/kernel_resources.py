@@ -41,7 +41,12 @@ def notes(so):
 if __name__ == "__main__":
     so = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(__file__), "..", "whisperx_amd", "libwxalign.so")
     pat = re.compile(sys.argv[2] if len(sys.argv) > 2 else "align_dp")
-    for o in notes(so):
+    # a sharded build links several code objects; the unbundler reads only the first, so read
+    # the build's objects (build/obj/<lib>/*.o) when they are there
+    import glob
+    objs = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "..", "build", "obj",
+                                         os.path.basename(so).replace(".so", ""), "*.o")))
+    for o in [x for f in (objs or [so]) for x in notes(f)]:
         if pat.search(o["name"]):
             print(f"{o['name'][:60]:60s} vgpr {o.get('vgpr_count'):>4} sgpr {o.get('sgpr_count'):>4} "
                   f"scratch {o.get('private_segment_fixed_size'):>5} lds {o.get('group_segment_fixed_size'):>6} "

@@ -35,6 +35,15 @@ KER(k_add8, R16("v_add_f32 v0, v0, v9\n v_add_f32 v1, v1, v9\n v_add_f32 v2, v2,
 KER(k_max4, R16("v_maximum3_f32 v0, v0, v9, v9\n v_maximum3_f32 v1, v1, v9, v9\n v_maximum3_f32 v2, v2, v9, v9\n v_maximum3_f32 v3, v3, v9, v9\n"), 64)
 KER(k_cmpaddc, R16("v_cmp_gt_f32 vcc, v0, v9\n v_addc_co_u32 v1, vcc, v1, v1, vcc\n"), 32)
 KER(k_salu_dep, R16("s_add_u32 s20, s20, 1\n"), 16)
+// fp64 / 64-bit integer chains (the column-0 routine's building blocks)
+KER(k_f64add, R16("v_add_f64 v[0:1], v[0:1], v[8:9]\n"), 16)
+KER(k_f64mul, R16("v_mul_f64 v[0:1], v[0:1], v[8:9]\n"), 16)
+KER(k_f64rnd, R16("v_rndne_f64 v[0:1], v[0:1]\n"), 16)
+KER(k_f64add4, R16("v_add_f64 v[0:1], v[0:1], v[8:9]\n v_add_f64 v[2:3], v[2:3], v[8:9]\n v_add_f64 v[4:5], v[4:5], v[8:9]\n v_add_f64 v[6:7], v[6:7], v[8:9]\n"), 64)
+KER(k_u64add, R16("v_add_co_u32 v0, vcc, v0, v9\n v_addc_co_u32 v1, vcc, v1, v9, vcc\n"), 32)
+KER(k_dpp64, R16("v_mov_b32_dpp v2, v0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_mov_b32_dpp v3, v1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_add_f64 v[0:1], v[0:1], v[2:3]\n"), 48)
+KER(k_dppu64, R16("v_mov_b32_dpp v2, v0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_mov_b32_dpp v3, v1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n v_add_co_u32 v0, vcc, v0, v2\n v_addc_co_u32 v1, vcc, v1, v3, vcc\n"), 64)
+KER(k_cvt64, R16("v_cvt_f64_f32 v[0:1], v2\n v_cvt_f32_f64 v2, v[0:1]\n"), 32)
 
 int main() {
     unsigned long long* d;
@@ -46,7 +55,10 @@ int main() {
         {"add->maximum3 chain", k_addmax1, 32}, {"dpp chain", k_dpp1, 16}, {"dpp->add chain", k_dppadd1, 32},
         {"add_dpp (fused) chain", k_dppaddf, 16}, {"add 2 chains", k_add2, 32}, {"add 4 chains", k_add4, 64},
         {"add 8 chains", k_add8, 128}, {"maximum3 4 chains", k_max4, 64}, {"cmp->addc pairs", k_cmpaddc, 32},
-        {"salu chain", k_salu_dep, 16}};
+        {"salu chain", k_salu_dep, 16}, {"f64 add chain", k_f64add, 16}, {"f64 mul chain", k_f64mul, 16},
+        {"f64 rndne chain", k_f64rnd, 16}, {"f64 add 4 chains", k_f64add4, 64}, {"u64 add (2 instr) chain", k_u64add, 32},
+        {"dpp64 + f64 add (3 instr)", k_dpp64, 48}, {"dpp64 + u64 add (4 instr)", k_dppu64, 64},
+        {"cvt f32->f64->f32 (2 instr)", k_cvt64, 32}};
     for (int wps : {1, 2, 4}) {
         printf("== %d wave(s) per SIMD (workgroup of %d waves on one CU)\n", wps, 4 * wps);
         for (auto& k : ks) {

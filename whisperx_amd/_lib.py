@@ -65,6 +65,7 @@ SIGNATURES = {
     "wx_backtrack": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64,
                                     _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "wx_merge_repeats": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "wx_column0_cumsum": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "wx_align_dp_workspace_bytes": (_sz, [_i32, _i64, _i64]),
     "wx_align_dp": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _i32, _i64, _i64, _i64,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -466,6 +467,18 @@ def merge_repeats(path_tok, path_time, path_prob, path_off, path_len, device):
         _check(lib.wx_merge_repeats(_ptr(path_tok), _ptr(path_time), _ptr(path_prob), _ptr(path_off), _ptr(path_len),
                                     S, _ptr(st), _ptr(ss), _ptr(se), _ptr(sc), _ptr(cnt), _stream(dev)))
     return st, ss, se, sc, cnt
+
+
+def column0_cumsum(em):
+    """Column 0 of get_trellis (alignment.py:367) as the fused DP computes it: the fp64 running
+    sums S(0..T) of em[:, 0] (a [T, V] fp32 device tensor), as a float64 device tensor."""
+    lib = load()
+    em = em.contiguous()
+    T, V = int(em.shape[0]), int(em.shape[1])
+    out = torch.empty(T + 1, dtype=torch.float64, device=em.device)
+    with torch.cuda.device(em.device):
+        _check(lib.wx_column0_cumsum(_ptr(em), T, V, _ptr(out), _stream(em.device)))
+    return out
 
 
 def binarize(scores_list, sw_geometry, onset: float, offset: float, max_duration: float,

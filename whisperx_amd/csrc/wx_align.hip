@@ -1074,6 +1074,25 @@ __global__ __launch_bounds__(kBinWG) void binarize_scan_kernel(BinScanArgs sa) {
 
 }  // namespace wx
 
+namespace wx {
+// Column 0 of get_trellis (alignment.py:367): S(t) = em[0, c] + ... + em[t - 1, c] in double,
+// row order, t = 0..T — the fused DP's own column-0 routine (col0_chunk: binade scan, else the
+// sequential chain), one wave.  Rows past T in the last chunk enter as 0 and feed only sums
+// past S(T), which are not stored.
+__global__ __launch_bounds__(kWave) void column0_cumsum_kernel(const float* __restrict__ em, int64_t T, int V,
+                                                               double* __restrict__ S) {
+    const int l = lane_id();
+    double acc = 0.0;
+    for (int64_t t0 = 0; t0 < T; t0 += kChunk) {
+        const int64_t t = t0 + (l & (kChunk - 1));
+        const float e = t < T ? em[t * V] : 0.0f;
+        const double a = col0_chunk(acc, e);
+        if (l < kChunk) S[t0 + l] = a;  // S(t0 + l), t0 + l < T
+    }
+    if (l == 0) S[T] = acc;
+}
+}  // namespace wx
+
 // ======================================================================================
 // C ABI
 namespace wx {
@@ -1361,6 +1380,16 @@ static int spin_limit() {
     if (e && e[0] >= '0' && e[0] <= '9') return std::min(atoi(e), kMaxSpin);
     return kMaxSpin;
 }
+// Split-arrival flags, read per call (tests and A/B): WX_SPLIT_FENCED=1 adds the release /
+// acquire fences to the write-through arrival, WX_SPLIT_XCD_SPREAD=1 spreads each segment's
+// parts over different XCDs.
+static int split_flags() {
+    auto on = [](const char* n) {
+        const char* e = getenv(n);
+        return e && e[0] == '1';
+    };
+    return (on("WX_SPLIT_FENCED") ? kArgFenced : 0) | (on("WX_SPLIT_XCD_SPREAD") ? kArgXcdSpread : 0);
+}
 
 size_t wx_align_dp_handoff_bytes(int32_t S, int64_t sum_T) { return xg_bytes(S, sum_T) + arrive_bytes(S); }
 
@@ -1416,6 +1445,7 @@ int wx_align_dp_ex(const float* em, const int64_t* em_off, int32_t V, const int3
     a.parts = split_parts(S, a.mode, mode);
     a.epoch = next_epoch();
     a.spin = spin_limit();
+    a.flags = split_flags();
     if (a.parts > 1 && !handoff) {  // workspace hand-off region: holds anything until zeroed
         const hipError_t e = hipMemsetAsync(a.xg, 0, wx_align_dp_handoff_bytes(S, sum_T), st);
         if (e != hipSuccess) return (int)e;
@@ -1552,6 +1582,13 @@ int wx_merge_repeats(const int32_t* path_tok, const int32_t* path_time, const fl
     a.seg_tok = seg_tok; a.seg_start = seg_start; a.seg_end = seg_end; a.seg_score = seg_score;
     a.seg_count = seg_count;
     hipLaunchKernelGGL(merge_repeats_kernel, dim3(S), dim3(kWave), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launch_status();
+}
+
+int wx_column0_cumsum(const float* em, int64_t T, int32_t V, double* S, void* stream) {
+    if (T < 0 || V < 1 || !S || (T > 0 && !em)) return WX_E_INVALID;
+    hipLaunchKernelGGL(column0_cumsum_kernel, dim3(1), dim3(kWave), 0, reinterpret_cast<hipStream_t>(stream), em, T,
+                       V, S);
     return launch_status();
 }
 

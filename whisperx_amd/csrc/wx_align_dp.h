@@ -106,6 +106,55 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, i
     return ((unsigned long long)hi << 32) | lo;
 }
 
+// Column 0's running sum over one 32-row chunk (alignment.py:366-370: torch's CPU cumsum
+// accumulates em[:, 0] in double, row by row).  Lane j converts em[t0 + j, 0] (one instruction
+// for the chunk), the doubles go through LDS and come back broadcast (16-byte reads, every lane
+// the same address), and at step j the lanes r > j add row j: an EXEC-masked v_add_f64 with a
+// scalar s_bitset0 retiring lane j + 1 after it.  Lane r (0..32) thus adds em[t0 + 0 .. r - 1, 0]
+// in row order onto S(t0) and nothing else — the sequential chain's additions exactly.  (Round
+// 5: two instructions per row instead of a conversion, a DPP shift and the add; config 2 50.8
+// -> 47.5 us.)
+__device__ __forceinline__ double col0_chain(double acc, float e) {
+    const int l = lane_id();
+    __shared__ __attribute__((aligned(16))) double c0d[kChunk];
+    if (l < kChunk) c0d[l] = (double)e;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (other lanes' writes, read below)
+    double dv[kChunk];
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) dv[j] = c0d[j];
+    double a = acc;
+    unsigned long long sv;
+#define WX_C0_STEP(J, BIT) "v_add_f64 %[a], %[a], %[d" #J "]\n\ts_bitset0_b64 exec, " #BIT "\n\t"
+#define WX_C0_BLOCK(B, J0, B1, B2, B3, B4, B5, B6, B7, B8)                                                      \
+    asm volatile("s_mov_b64 %[sv], exec\n\t"                                                                  \
+                 "s_mov_b32 exec_lo, %[mlo]\n\t"                                                              \
+                 "s_mov_b32 exec_hi, 1\n\t" WX_C0_STEP(0, B1) WX_C0_STEP(1, B2) WX_C0_STEP(2, B3)              \
+                     WX_C0_STEP(3, B4) WX_C0_STEP(4, B5) WX_C0_STEP(5, B6) WX_C0_STEP(6, B7)                   \
+                         WX_C0_STEP(7, B8) "s_mov_b64 exec, %[sv]\n\t"                                        \
+                 : [a] "+v"(a), [sv] "=&s"(sv)                                                                 \
+                 : [mlo] "s"((unsigned)(0xFFFFFFFFu << ((J0) + 1))), [d0] "v"(dv[(J0)]),                      \
+                   [d1] "v"(dv[(J0) + 1]), [d2] "v"(dv[(J0) + 2]), [d3] "v"(dv[(J0) + 3]),                     \
+                   [d4] "v"(dv[(J0) + 4]), [d5] "v"(dv[(J0) + 5]), [d6] "v"(dv[(J0) + 6]),                     \
+                   [d7] "v"(dv[(J0) + 7]))
+    // block b: rows 8b .. 8b + 7, lanes 8b + 1 .. 32 active at its start (exec_hi = lane 32)
+    WX_C0_BLOCK(0, 0, 1, 2, 3, 4, 5, 6, 7, 8);
+    WX_C0_BLOCK(1, 8, 9, 10, 11, 12, 13, 14, 15, 16);
+    WX_C0_BLOCK(2, 16, 17, 18, 19, 20, 21, 22, 23, 24);
+    WX_C0_BLOCK(3, 24, 25, 26, 27, 28, 29, 30, 31, 32);
+#undef WX_C0_BLOCK
+#undef WX_C0_STEP
+    return a;
+}
+
+// One chunk of column 0's running sum: lane l (0..31) holds e = em[t0 + l, 0] (lanes 32..63:
+// any copy), acc = S(t0) (uniform).  Returns S(t0 + l) on lane l and advances acc to S(t0 + 32)
+// (lane 32's sum, by v_readlane: no LDS round trip).
+__device__ __forceinline__ double col0_chunk(double& acc, float e) {
+    const double a = col0_chain(acc, e);
+    acc = __builtin_bit_cast(double, readlane64(__builtin_bit_cast(unsigned long long, a), kChunk));
+    return a;
+}
+
 // Cell values live in an ext_vector so that the one dynamic (wave-uniform) index of the
 // step — the slot holding column N — lowers to s_set_gpr_idx_on/v_mov instead of scratch.
 template <int C>
@@ -451,12 +500,14 @@ __device__ __forceinline__ uint64_t granule_load(const uint64_t* g) {
 // bits) nor the acquire (MI355X_MICROARCH.md, "Valid forms": one lane per storing workgroup
 // adds to one counter after every storing wave's vmcnt(0) wait and a workgroup barrier, the
 // workgroup whose add came last loads after it returned, its other waves after a barrier;
-// 4- and 16-byte sc1 stores and loads).  -DWX_SPLIT_FENCED builds the fenced protocol.
-#ifdef WX_SPLIT_FENCED
-constexpr bool kSplitWT = false;
-#else
+// 4- and 16-byte sc1 stores and loads).  That table is measured behaviour on gfx950 / ROCm
+// 7.2 (the guide's hand-off table, row 1), not an architectural guarantee, so the launch flag
+// kArgFenced (WX_SPLIT_FENCED=1) adds the agent-scope release and acquire on top of the
+// write-through stores — the memory model's own protocol — and the parity tests compare the
+// two bit for bit with the parts of every segment spread over different XCDs (kArgXcdSpread).
 constexpr bool kSplitWT = true;
-#endif
+constexpr int kArgFenced = 1;     // AlignArgs::flags: release/acquire at the split arrival
+constexpr int kArgXcdSpread = 2;  // AlignArgs::flags: parts of a segment on different XCDs (tests)
 // Register-resident split kernels only (C = 1, config 2): in the C > 1 split kernels the
 // consumer's hand-off waits drain vmcnt inside the chain, and write-through stores take longer
 // to drain (A/B, 64 x T = 2999, N ~ 900: fenced 166 us, write-through 178 us).
@@ -1042,72 +1093,18 @@ struct Forward {
     // tr[t][0] + em[t, tok[0]] for the rows of chunk q (the column-1 wave's lane-0 operand),
     // into column VS of the chunk's quad buffer.  tr[t][0] (alignment.py:367-370): 0 at t = 0,
     // fp32 of the fp64 sum of em[0..t-1, 0] (torch CPU cumsum accumulates in double, in row
-    // order), +inf in the last N rows.
-    // The prefix sums are formed lane-parallel without reassociating: lane 32 + i starts with
-    // em[t0 + i, 0], lanes 0..31 with +0, and at step j every lane adds its value and then takes
-    // its right neighbour's (DPP wave_shl:1, zero-filled).  Lane r (0..32) so adds exactly
-    // em[t0 + 0 .. r - 1, 0], in row order, into the running sum S(t0): it ends holding S(t0 + r)
-    // — the same fp64 additions, in the same order, as the sequential chain — and adding +0 is
-    // exact (the sum is never -0).  Three VALU per row, no exec juggling (a uniform chain with
-    // per-row conversions and broadcasts measured ~38 cycles per row, slower than the DP
-    // chunk it feeds).
+    // order), +inf in the last N rows.  The sums: col0_chunk.
     __device__ __forceinline__ static void col0_pre(int q, const SegDesc& d, float* buf, int tok0, double& acc) {
         const int T = d.T, N = d.N;
         const int l = lane_id();
         const int rr = l & 31;
-        const float e = buf[(rr >> 2) * kQS + (rr & 3)];  // column 0 of row rr
-#ifdef WX_COL0_DPP
-        float x = l >= 32 ? e : 0.0f;
-        double a = acc;
-#pragma unroll
-        for (int j = 0; j < kChunk; ++j) {
-            a += (double)x;
-            x = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x130 /* wave_shl:1 */,
-                                                                   0xF, 0xF, true));
-        }
-#else
-        // Round 5: the same sums with the row values uniform.  Lane j converts em[t0 + j, 0]
-        // (one instruction for the chunk), the doubles go through LDS and come back broadcast
-        // (16-byte reads, every lane the same address), and at step j the lanes r > j add row
-        // j: an EXEC-masked v_add_f64 with a scalar s_bitset0 retiring lane j + 1 after it.  Lane
-        // r thus adds em[t0 + 0 .. r - 1, 0] in row order onto S(t0) and nothing else — the
-        // sequential chain's additions exactly, no +0 terms.  Two instructions per row instead
-        // of a conversion, a DPP shift and the add (the column-0 helper paced part 0: with half
-        // rows — a timing experiment with wrong results — config 2 ran 50.8 -> 46.1 us; this form:
-        // 50.8 -> 47.5 us, bit-identical).  -DWX_COL0_DPP builds the previous form.
-        __shared__ __attribute__((aligned(16))) double c0d[kChunk];
-        if (l < kChunk) c0d[l] = (double)e;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (other lanes' writes, read below)
-        double dv[kChunk];
-#pragma unroll
-        for (int j = 0; j < kChunk; ++j) dv[j] = c0d[j];
-        double a = acc;
-        unsigned long long sv;
-#define WX_C0_STEP(J, BIT) "v_add_f64 %[a], %[a], %[d" #J "]\n\ts_bitset0_b64 exec, " #BIT "\n\t"
-#define WX_C0_BLOCK(B, J0, B1, B2, B3, B4, B5, B6, B7, B8)                                                      \
-        asm volatile("s_mov_b64 %[sv], exec\n\t"                                                              \
-                     "s_mov_b32 exec_lo, %[mlo]\n\t"                                                          \
-                     "s_mov_b32 exec_hi, 1\n\t" WX_C0_STEP(0, B1) WX_C0_STEP(1, B2) WX_C0_STEP(2, B3)          \
-                         WX_C0_STEP(3, B4) WX_C0_STEP(4, B5) WX_C0_STEP(5, B6) WX_C0_STEP(6, B7)               \
-                             WX_C0_STEP(7, B8) "s_mov_b64 exec, %[sv]\n\t"                                    \
-                     : [a] "+v"(a), [sv] "=&s"(sv)                                                             \
-                     : [mlo] "s"((unsigned)(0xFFFFFFFFu << ((J0) + 1))), [d0] "v"(dv[(J0)]),                  \
-                       [d1] "v"(dv[(J0) + 1]), [d2] "v"(dv[(J0) + 2]), [d3] "v"(dv[(J0) + 3]),                 \
-                       [d4] "v"(dv[(J0) + 4]), [d5] "v"(dv[(J0) + 5]), [d6] "v"(dv[(J0) + 6]),                 \
-                       [d7] "v"(dv[(J0) + 7]))
-        // block b: rows 8b .. 8b + 7, lanes 8b + 1 .. 32 active at its start (exec_hi = lane 32)
-        WX_C0_BLOCK(0, 0, 1, 2, 3, 4, 5, 6, 7, 8);
-        WX_C0_BLOCK(1, 8, 9, 10, 11, 12, 13, 14, 15, 16);
-        WX_C0_BLOCK(2, 16, 17, 18, 19, 20, 21, 22, 23, 24);
-        WX_C0_BLOCK(3, 24, 25, 26, 27, 28, 29, 30, 31, 32);
-#undef WX_C0_BLOCK
-#undef WX_C0_STEP
-#endif
-        acc = __shfl(a, 32);  // S(t0 + 32): the next chunk's start (uniform)
+        // both operands of the row read up front: one LDS round trip instead of two
+        const float e = buf[(rr >> 2) * kQS + (rr & 3)];              // em[t, 0]
+        const float et = buf[(rr >> 2) * kQS + 4 * tok0 + (rr & 3)];  // em[t, tok[0]]
+        const double a = col0_chunk(acc, e);
         if (l < 32) {
             const int t = q * kChunk + l;
-            const float v = col0_value(t, a, T, N) + buf[(l >> 2) * kQS + 4 * tok0 + (l & 3)];
-            buf[(l >> 2) * kQS + 4 * VS + (l & 3)] = v;
+            buf[(l >> 2) * kQS + 4 * VS + (l & 3)] = col0_value(t, a, T, N) + et;
         }
     }
     // Staging of the quad layout.  Rows are first copied row-major into a ring of kRing raw
@@ -2669,6 +2666,7 @@ struct AlignArgs {
     uint64_t* xg;    // workspace: hand-off granules, (floor(row0/32) + seg + q) * 3 * 40
     uint64_t* arrive;// workspace: per-segment arrival counters {count, epoch} (split_arrive)
     int spin;        // split launches: hand-off re-reads before a part counts as lost
+    int flags;       // split launches: kArgFenced | kArgXcdSpread (WX_SPLIT_FENCED, WX_SPLIT_XCD_SPREAD)
 };
 
 // Per-segment arrival of a split segment's parts.  The counter is one 8-byte word,
@@ -2725,22 +2723,16 @@ __device__ __forceinline__ bool prepare_colmap(ColMapLds<VS>& m, ColMap& cm, con
 // block's rows load while a block computes) where that keeps the LDS of a workgroup within its
 // share at 4 waves per SIMD (VS == 32, and the one-wave kernels' two forward buffers), else one
 // per walker wave (rows loaded at use, the next block's warmed into the L2).
+// (One slot per walker wave everywhere measured slower in round 5.)
 template <int VS, int W>
-constexpr int kCkSlots =
-#ifdef WX_CK1
-    W == 1 ? 2 : W;
-#else
-    (W == 1 || VS == 32) ? 2 * W : W;
-#endif
+constexpr int kCkSlots = (W == 1 || VS == 32) ? 2 * W : W;
 
 // Split kernels: waves per workgroup.  Beyond the W DP waves and the two helpers, the rest
 // only keep the forward's barrier count and then walk speculative segments (walk_spec: more
 // walkers, shorter segments).  177 VGPRs allow two waves per SIMD: 8 (12 waves = 168 VGPRs
-// spilled 33 in the register-resident forward).  (-DWX_SPLIT_WAVES=6: no extra walkers.)
-#ifndef WX_SPLIT_WAVES
-#define WX_SPLIT_WAVES 8
-#endif
-constexpr int kSplitWaves = WX_SPLIT_WAVES;
+// spilled 33 in the register-resident forward).  (6 waves, no extra walkers: config 2
+// 51.4 -> 53.3 us in round 5.)
+constexpr int kSplitWaves = 8;
 constexpr int kQ0LdsFrames = 4096;  // Split::q0l rows (longer segments: fill_q0 after the walk)
 
 template <int C, int VS, int W, int H, bool SP = false, int XW = 0>
@@ -2769,10 +2761,13 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     // Split grids: block b = ((s / 8) * P + p) * 8 + s % 8, so the parts of segment s share
     // b % 8 — one XCD under the observed round-robin dispatch — and read its emission rows
     // through one L2.  (Placement is a speed matter only; part p - 1 has the lower block
-    // index either way, so it starts no later than part p.)
-    const int seg = SP ? ((int)blockIdx.x / kXcdStride / P) * kXcdStride + (int)blockIdx.x % kXcdStride
-                       : (int)blockIdx.x;
+    // index either way, so it starts no later than part p.)  kArgXcdSpread (tests) puts part p
+    // at b % 8 = (s + p) % 8 instead: every part of a segment on another XCD.
     const int part = SP ? ((int)blockIdx.x / kXcdStride) % P : 0;
+    const int xslot = (int)blockIdx.x % kXcdStride;
+    const int seg = SP ? ((int)blockIdx.x / kXcdStride / P) * kXcdStride +
+                             ((a.flags & kArgXcdSpread) ? (xslot - part) & (kXcdStride - 1) : xslot)
+                       : (int)blockIdx.x;
     if (SP && seg >= a.S) return;  // grid padded to a multiple of 8 segments
     const SegDesc d = load_desc(a.em_off, a.tok_off, a.blank_id, seg);
     const int want = (SP || a.parts > 1) ? launch_split_bucket(d.N, a.parts, a.split_id) : bucket_id(d.N, a.mode);
@@ -2824,14 +2819,15 @@ __device__ __forceinline__ void align_dp_body(const AlignArgs& a) {
     if (SP && !slow) {  // release this part's bits / column-N history; the last part to arrive goes on
         if (lane == 0) {
             // (WT: every wave's stores drained above, then the barrier: no release)
-            if (!WT) {
+            const bool fenced = !WT || (a.flags & kArgFenced);
+            if (fenced) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 wait_vm();
             }
             const unsigned w = split_arrive(a.arrive + seg, a.epoch, tsb[2] != 0);
             tsb[0] = ((w & 0x7Fu) == (unsigned)P) ? 1 + (int)((w >> 7) & 1u) : 0;
             if (tsb[0]) {
-                if (!WT) {  // (WT: the walk reads the parts' words with sc1 loads)
+                if (fenced) {  // (WT: the walk reads the parts' words with sc1 loads)
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     wait_vm();
                 }

@@ -347,14 +347,7 @@ struct AttnArgs {
     int nseg;
 };
 
-#ifndef WX_ATTN_SPLIT
-#define WX_ATTN_SPLIT 4
-#endif
-constexpr int kAttnSplit = WX_ATTN_SPLIT;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
-
-#ifndef WX_ATTN_XCD
-#define WX_ATTN_XCD 1
-#endif
+constexpr int kAttnSplit = 4;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
 
 // amdgpu_waves_per_eu(2): the occupancy it gets anyway (242 registers), stated so the allocator
 // keeps everything in 203 VGPRs instead of splitting 194 / 48 with AGPR copies (A/B: 1-2% faster).
@@ -370,13 +363,11 @@ __global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2)))
     // 1-D grid, block L runs on XCD L % 8 (round-robin dispatch): hand each XCD a contiguous
     // run of (head, query tile) units, so the blocks sharing one head's K / V (768 KB at
     // T = 1499) meet in one XCD's L2 instead of all eight
-    unsigned w;
-    if (WX_ATTN_XCD) {
+    // (round 4 A/B: the plain blockIdx order was 1-2% slower)
+    const unsigned w = [] {
         const unsigned L = blockIdx.x, n = gridDim.x, x = L % 8, i = L / 8, q = n / 8, r = n % 8;
-        w = x * q + min(x, r) + i;
-    } else {
-        w = blockIdx.x;
-    }
+        return x * q + min(x, r) + i;
+    }();
     if (PACKED) {
         // the segment owning unit w: the last s with seg_units[s] <= w (empty segments own no
         // units, so the last such s is never one of them)

@@ -77,21 +77,30 @@ def _parse_cpulist(text: str) -> List[int]:
     return out
 
 
-def _visible(ids: List[int], var: str) -> List[int]:
-    v = os.environ.get(var, "").strip()
-    if not v:
-        return ids
-    try:
-        return [ids[int(x)] for x in v.split(",") if x.strip() != ""]
-    except (ValueError, IndexError):  # UUIDs or out-of-range entries: cannot map, keep all
-        return ids
+def _visible(ids: List[int]) -> Optional[List[int]]:
+    """The GPUs this process sees, as ROCr and HIP select them: ROCR_VISIBLE_DEVICES first, then
+    HIP_VISIBLE_DEVICES, or CUDA_VISIBLE_DEVICES only when HIP_VISIBLE_DEVICES is unset (HIP
+    honours one of the two, it does not compose them).  None when an entry cannot be mapped to
+    a KFD GPU (a UUID, an out-of-range index): the caller then has no reliable GPU -> node map."""
+    for names in (("ROCR_VISIBLE_DEVICES",), ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")):
+        v = next((os.environ[n] for n in names if os.environ.get(n, "").strip()), None)
+        if v is None:
+            continue
+        try:
+            ids = [ids[int(x)] for x in v.split(",") if x.strip() != ""]
+        except (ValueError, IndexError):
+            return None
+    return ids
 
 
-def host_topology(sysfs: str = "/sys") -> Optional[dict]:
+def host_topology(sysfs: str = "/sys", visible_only: bool = True) -> Optional[dict]:
     """{"gpu_nodes": NUMA node of each visible GPU in HIP's order, "node_cpus": {node: [cpus]}}
     from the KFD topology (GPU agents in node order, as ROCr enumerates them; PCI location ->
-    the device's numa_node) filtered by ROCR_/HIP_/CUDA_VISIBLE_DEVICES, or None when the host
-    does not expose it.  Reads sysfs only: no HIP call, so it can run before pinning."""
+    the device's numa_node) filtered by ROCR_/HIP_/CUDA_VISIBLE_DEVICES (_visible), or None when
+    the host does not expose it or the visibility list cannot be mapped.  visible_only=False
+    keeps every GPU the KFD lists: the node's layout even when this process sees fewer GPUs
+    (the host-share leg models rank 0 of an 8-GPU node on one visible GPU).  Reads sysfs only:
+    no HIP call, so it can run before pinning."""
     base = os.path.join(sysfs, "class/kfd/kfd/topology/nodes")
     try:
         nodes = sorted(int(n) for n in os.listdir(base) if n.isdigit())
@@ -113,8 +122,8 @@ def host_topology(sysfs: str = "/sys") -> Optional[dict]:
                 gpus.append(int(f.read().strip()))
         except (OSError, ValueError):
             gpus.append(-1)
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        gpus = _visible(gpus, var)
+    if visible_only:
+        gpus = _visible(gpus)
     if not gpus or any(g < 0 for g in gpus):
         return None
     node_cpus = {}
@@ -145,30 +154,52 @@ def rank_cpus_numa(cpus: Sequence[int], local_rank: int, local_world: int, topo:
 
 
 def pin_rank(local_rank: Optional[int] = None, local_world: Optional[int] = None,
-             topology: Optional[dict] = "auto") -> dict:
+             topology: Optional[dict] = "auto", sysfs: str = "/sys") -> dict:
     """Pin this rank to its disjoint CPU slice — on its GPU's NUMA node when the host exposes
     the topology (host_topology; `topology` overrides it, None disables it) — and size torch's
     intra-op pool to its share of the thread budget.  Call before any GPU work (HIP's runtime
     threads inherit the affinity).  Defaults: LOCAL_RANK / LOCAL_WORLD_SIZE from torchrun.
-    Returns {"cpus", "threads", "numa"}."""
+    When this process sees fewer GPUs than there are ranks (one GPU modelling rank 0 of a node,
+    or ranks sharing GPUs), the node's full KFD GPU list stands in: rank r <-> the node's GPU r
+    ("numa_source": "node_model").  Returns {"cpus", "threads", "numa", "numa_source",
+    "numa_reason"} — the last says why "numa" is None."""
     lr = int(os.environ.get("LOCAL_RANK", "0")) if local_rank is None else int(local_rank)
     lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1")) if local_world is None else int(local_world)
     budget = thread_budget()
     if not hasattr(os, "sched_getaffinity"):
         threads = max(1, budget // max(lw, 1))
         torch.set_num_threads(threads)
-        return {"cpus": None, "threads": threads, "numa": None}
-    topo = host_topology() if topology == "auto" else topology
+        return {"cpus": None, "threads": threads, "numa": None, "numa_source": None,
+                "numa_reason": "no sched_getaffinity"}
+    source, reason = None, None
+    if topology == "auto":
+        topo, source = host_topology(sysfs), "visible"
+        if topo is None or len(topo["gpu_nodes"]) < lw:
+            seen = "no KFD topology or unmappable *_VISIBLE_DEVICES" if topo is None else \
+                f"{len(topo['gpu_nodes'])} visible GPU(s) for {lw} ranks"
+            node = host_topology(sysfs, visible_only=False)
+            if node is not None and len(node["gpu_nodes"]) >= lw:
+                topo, source = node, "node_model"
+            else:
+                topo, source = None, None
+                reason = seen + ("" if node is None else f"; the KFD lists {len(node['gpu_nodes'])} GPU(s)")
+    else:
+        topo, source = topology, ("given" if topology else None)
+        reason = None if topology else "topology disabled"
     aff = os.sched_getaffinity(0)
     mine = rank_cpus_numa(aff, lr, lw, topo)
     numa = None
     if topo and len(topo["gpu_nodes"]) > lr and set(mine) <= set(topo["node_cpus"].get(topo["gpu_nodes"][lr], [])):
         numa = topo["gpu_nodes"][lr]
+    elif topo:
+        reason = "the process affinity misses a rank's NUMA node: plain slices"
+    if numa is None:
+        source = None
     if mine:
         os.sched_setaffinity(0, mine)
     threads = max(1, min(len(mine) or 1, budget // max(lw, 1)))
     torch.set_num_threads(threads)
-    return {"cpus": mine, "threads": threads, "numa": numa}
+    return {"cpus": mine, "threads": threads, "numa": numa, "numa_source": source, "numa_reason": reason}
 
 
 def lpt_plan(durations: Sequence[float], worlds=(1, 2, 4, 8)) -> dict:
