@@ -575,6 +575,19 @@ def mae_e2e(device, n_seg=4, seed=7, large=False, seg_s=30.0):
             "vs": "reference CPU align() path (CPU forward + CPU DP), same weights and audio"}
 
 
+def config5_inputs(device, n_seg=8, seed=5):
+    """config5_leg's align() inputs: (segments, audio, large-xlsr-shaped model, metadata)."""
+    from whisperx_amd import synthetic
+
+    model = _w2v_large(device, seed)
+    meta = {"language": "de", "dictionary": synthetic.de_dictionary(), "type": "huggingface"}
+    tr = synthetic.Transcriber(seed, letters=synthetic.DE_LETTERS)
+    segs = tr.segments([{"start": 60.0 * k, "end": 60.0 * (k + 1)} for k in range(n_seg)])
+    g = torch.Generator().manual_seed(seed)
+    audio = torch.randn(int(60 * n_seg * 16000), generator=g) * 0.1
+    return segs, audio, model, meta
+
+
 def config5_leg(device, n_seg=8, seed=5, cpu_budget_s=20.0, dp_steps=20):
     """BASELINE config 5: German wav2vec2-large-xlsr-shaped model (24 x 1024, layer-norm feature
     encoder, stable layer norm; random weights), V = 40, long-form 60 s segments (T = 2999).
@@ -585,16 +598,11 @@ def config5_leg(device, n_seg=8, seed=5, cpu_budget_s=20.0, dp_steps=20):
     (c) the reference-structured CPU align() (CPU forward + TorchPort DP + host aggregation) on
         one 60 s clip at every usable host thread, repeated for ~cpu_budget_s."""
     import whisperx_amd
-    from whisperx_amd import _lib, synthetic
+    from whisperx_amd import _lib
 
     out = {}
-    model = _w2v_large(device, seed)
-    dictionary, letters = synthetic.de_dictionary(), synthetic.DE_LETTERS
-    meta = {"language": "de", "dictionary": dictionary, "type": "huggingface"}
-    tr = synthetic.Transcriber(seed, letters=letters)
-    segs = tr.segments([{"start": 60.0 * k, "end": 60.0 * (k + 1)} for k in range(n_seg)])
-    g = torch.Generator().manual_seed(seed)
-    audio = torch.randn(int(60 * n_seg * 16000), generator=g) * 0.1
+    segs, audio, model, meta = config5_inputs(device, n_seg, seed)
+    dictionary = meta["dictionary"]
     whisperx_amd.align([dict(x) for x in segs[:2]], model, meta, audio, device)  # warm-up
     torch.cuda.synchronize()
     st0 = _dp_stats()

@@ -133,3 +133,52 @@ def test_np_round3_matches_numpy_scalar_round():
         got = alignment._np_round3(np.float64(v))
         assert type(got) is type(ref)
         assert (got == ref and math.copysign(1, got) == math.copysign(1, ref)) or (ref != ref and got != got), (v, got, ref)
+
+
+def test_has_alignable_matches_prepare():
+    """align() decides which segments get a forward with _has_alignable before _prepare runs:
+    it must agree with _prepare's clean_char on every text (stripped range, lower-casing,
+    ' ' -> '|' in languages with spaces, multi-char lower-case forms)."""
+    from whisperx_amd import alignment
+
+    rng = np.random.default_rng(5)
+    pool = list("abc ABC|.,!?-'♪123 \t\nİßÅé日本")
+    dicts = [{"a": 1, "|": 2}, {"b": 1}, {"i̇": 1, "x": 2}, {"日": 1}, {"|": 1}, {}]
+    for _ in range(3000):
+        text = "".join(rng.choice(pool, int(rng.integers(0, 12))))
+        d = dicts[int(rng.integers(0, len(dicts)))]
+        lang = ["en", "ja", "de"][int(rng.integers(0, 3))]
+        seg = {"text": text}
+        alignment._prepare(seg, d, lang)
+        assert alignment._has_alignable(text, d, lang) == (len(seg["clean_char"]) > 0), (text, d, lang)
+
+
+def test_align_runs_no_forward_for_segments_it_skips(cpu_align, capsys):
+    """A segment with no alignable char (music, digits, a script the model lacks) and one past
+    the audio get no forward (the reference never calls the model for them,
+    alignment.py:185-202): the fake model holds logits for the two alignable segments only."""
+    from align_helpers import FakeCTC
+
+    rng = np.random.default_rng(3)
+    d = {"<pad>": 0, "|": 1, "a": 2, "b": 3}
+    T = 99  # frames of a 2 s segment
+
+    def peaky(n_tok):
+        lg = rng.standard_normal((T, 4)).astype(np.float32)
+        lg[:, 0] += 6
+        fr = np.sort(rng.choice(np.arange(1, T - 1), n_tok, replace=False))
+        lg[fr, rng.integers(1, 4, n_tok)] += 12
+        return lg
+
+    model = FakeCTC([peaky(5), peaky(2)])
+    segs = [{"start": 0.0, "end": 2.0, "text": "ab ba"}, {"start": 2.0, "end": 4.0, "text": " ♪123♪ "},
+            {"start": 4.0, "end": 6.0, "text": "ab"}, {"start": 9.0, "end": 10.0, "text": "ab"}]
+    out = cpu_align(segs, model, {"language": "en", "dictionary": d, "type": "huggingface"},
+                    np.zeros(6 * 16000, np.float32), "cpu")
+    assert not model.queue
+    assert [s["text"] for s in out["segments"]] == ["ab ba", " ♪123♪ ", "ab", "ab"]
+    assert out["segments"][1]["words"] == [] and out["segments"][3]["words"] == []
+    assert len(out["segments"][0]["words"]) == 2 and len(out["segments"][2]["words"]) == 1
+    msg = capsys.readouterr().out
+    assert "no characters in this segment found in model dictionary" in msg
+    assert "original start time longer than audio duration" in msg

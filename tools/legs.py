@@ -1,9 +1,11 @@
 """One bench leg in isolation, for rocprofv3 runs (development tool): the program after
 `rocprofv3 ... --` runs exactly this leg's kernel K times after W warm-ups.
 
-    python tools/legs.py cfg2|sat3000|trellis3000|vad1h [--steps K] [--warmup W]
+    python tools/legs.py cfg2|cfg5|sat3000|trellis3000|vad1h|e2e|e2e5 [--steps K] [--warmup W]
 
 cfg2: the headline step (64 x T=1499, V=32, wx_align_dp in the default shape);
+cfg5: BASELINE config 5's DP (64 x T=2999, V=40, N~U[850,950], default shape);
+e2e / e2e5: align() end to end, 16 x 30 s wav2vec2-base / 8 x 60 s large-xlsr shape (config 5);
 sat3000: 2048 x T=2999, V=32, N~U[850,951], wx_align_dp (throughput shape);
 trellis3000: get_trellis materialised (wx_trellis) on the sat3000 batch;
 vad1h: the VAD producer (PyanNet-shaped segmentation forward + wx_vad_aggregate) over 1 h."""
@@ -44,10 +46,13 @@ def main():
         torch.cuda.synchronize()
         print(f"vad1h: {e0.elapsed_time(e1) / a.steps:.4f} ms per launch, 1 h of audio", flush=True)
         return
-    if a.leg == "e2e":  # align() end to end on 16 x 30 s segments (bench.e2e_align's inputs)
+    if a.leg in ("e2e", "e2e5"):  # align() end to end (bench.e2e_align's / config5_leg's inputs)
         import bench
 
-        segs, audio, model, meta = bench.e2e_leg_inputs(dev)
+        if a.leg == "e2e":
+            segs, audio, model, meta = bench.e2e_leg_inputs(dev)
+        else:
+            segs, audio, model, meta = bench.config5_inputs(dev)
         import whisperx_amd
 
         for _ in range(max(1, a.warmup)):
@@ -69,6 +74,8 @@ def main():
         return
     if a.leg == "cfg2":
         ems, toks = make_batch(64, 1499, 32, 300, 500, 1000, dev)
+    elif a.leg == "cfg5":
+        ems, toks = make_batch(64, 2999, 40, 850, 950, 55, dev)
     else:
         ems, toks = make_batch(2048, 2999, 32, 850, 951, 78, dev)
     b = _lib.Batch(ems, toks, [0] * len(ems), device=dev)

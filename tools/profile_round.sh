@@ -29,6 +29,7 @@ dp_legs() {
     timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $RX --output-format csv -d "$O/fetch" -o p -- python3 "$R/tools/legs.py" $LEG --steps 5 > "$O/fetch.log" 2>&1 || { echo "$LEG fetch failed"; return 1; }
     timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $RX --output-format csv -d "$O/write" -o p -- python3 "$R/tools/legs.py" $LEG --steps 5 > "$O/write.log" 2>&1 || { echo "$LEG write failed"; return 1; }
     timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM --kernel-include-regex $RX --output-format csv -d "$O/sq" -o p -- python3 "$R/tools/legs.py" $LEG --steps 5 > "$O/sq.log" 2>&1 || { echo "$LEG sq failed"; return 1; }
+    timeout -s KILL 180 rocprofv3 --pmc SQ_LDS_CMD_FIFO_FULL SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS --kernel-include-regex $RX --output-format csv -d "$O/lds" -o p -- python3 "$R/tools/legs.py" $LEG --steps 5 > "$O/lds.log" 2>&1 || { echo "$LEG lds failed"; return 1; }
     grep "ms per launch" "$O/stats.log"
   done
 }
@@ -43,13 +44,14 @@ stats_leg() {  # kernel stats of one tools/legs.py leg into gpurun_out/prof_ROUN
 case $MODE in
   profile)
     RND=${1:?round}; shift
-    LEGS=${*:-cfg2 sat3000 trellis3000}
+    LEGS=${*:-cfg2 cfg5 sat3000 trellis3000}
     dp_legs "$RND" $LEGS || exit 1
     stats_leg "$RND" vad1h || exit 1
     stats_leg "$RND" e2e || exit 1
+    stats_leg "$RND" e2e5 || exit 1
     cd "$R" && python3 tools/summarize_profiles.py "$RND" > "gpurun_out/summarize_$RND.log" 2>&1 || { echo "summarize failed"; tail -20 "gpurun_out/summarize_$RND.log"; exit 1; }
     mkdir -p "gpurun_out/profiles_$RND" && cp profiles/${RND}_* "gpurun_out/profiles_$RND/"
-    for LEG in vad1h e2e; do
+    for LEG in vad1h e2e e2e5; do
       find "gpurun_out/prof_$RND/$LEG/stats" -name "*kernel_stats.csv" -exec cp {} "gpurun_out/profiles_$RND/${RND}_${LEG}_kernel_stats.csv" \;
     done
     rm -rf "gpurun_out/prof_$RND"

@@ -15,8 +15,10 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LEGS = {"cfg2": (64, 1499, 300, 500, 1000), "sat3000": (2048, 2999, 850, 951, 78),
-        "trellis3000": (2048, 2999, 850, 951, 78)}
+LEGS = {"cfg2": (64, 1499, 300, 500, 1000, 32), "cfg5": (64, 2999, 850, 950, 55, 40),
+        "sat3000": (2048, 2999, 850, 951, 78, 32), "trellis3000": (2048, 2999, 850, 951, 78, 32)}
+# bench.py's pmc_traffic() reads these (newest round first, matched by kernel name)
+TRAFFIC_FILES = {"cfg2": "pmc_traffic.json", "cfg5": "pmc_traffic_cfg5.json", "sat3000": "pmc_traffic_sat3000.json"}
 
 
 def Ns(S, T, lo, hi, seed, V=32):
@@ -49,7 +51,7 @@ def main():
     rnd = sys.argv[1]
     base = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
     summary = {}
-    for leg, (S, T, lo, hi, seed) in LEGS.items():
+    for leg, (S, T, lo, hi, seed, V) in LEGS.items():
         d = os.path.join(base, leg)
         stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
         if not stats:
@@ -59,13 +61,13 @@ def main():
         rows = [r for r in csv.DictReader(open(stats[0])) if ksub in r["Name"]]
         top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
         avg_ns = float(top["AverageNs"])
-        n = Ns(S, T, lo, hi, seed)
+        n = Ns(S, T, lo, hi, seed, V)
         if leg == "trellis3000":
-            alg = sum(4 * T * 32 + 4 * x + 4 * (T + 1) * (x + 1) for x in n)
+            alg = sum(4 * T * V + 4 * x + 4 * (T + 1) * (x + 1) for x in n)
         else:
-            alg = sum(4 * T * 32 + 4 * x + (T * x) // 8 + 16 * x for x in n)
+            alg = sum(4 * T * V + 4 * x + (T * x) // 8 + 16 * x for x in n)
         pmc = {}
-        for sub in ("fetch", "write", "sq"):
+        for sub in ("fetch", "write", "sq", "lds"):
             v, cnt = per_dispatch(os.path.join(d, sub), ksub)
             pmc.update(v)
         fetch_b = 2 * pmc.get("FETCH_SIZE", float("nan")) * 1024  # gfx950: FETCH_SIZE counts half
@@ -84,10 +86,16 @@ def main():
         sq = summary[leg]["sq"]
         if sq.get("SQ_BUSY_CYCLES") and sq.get("SQ_ACTIVE_INST_VALU"):
             summary[leg]["valu_active_per_busy_cycle"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_BUSY_CYCLES"]
-        if leg == "cfg2":
-            with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic.json"), "w") as fh:
+        if sq.get("SQ_BUSY_CYCLES") and sq.get("SQ_LDS_CMD_FIFO_FULL") is not None:
+            summary[leg]["lds_cmd_fifo_full_per_busy_cycle"] = sq["SQ_LDS_CMD_FIFO_FULL"] / sq["SQ_BUSY_CYCLES"]
+        if sq.get("SQ_INSTS_VALU"):  # VALU instructions per 64 cells of one step (a wave64 step of 64 cells)
+            summary[leg]["valu_per_64_cell_step"] = sq["SQ_INSTS_VALU"] / (sum(T * x for x in n) / 64.0)
+        if leg in TRAFFIC_FILES:
+            with open(os.path.join(ROOT, "profiles", f"{rnd}_{TRAFFIC_FILES[leg]}"), "w") as fh:
                 json.dump({"kernel": top["Name"], "command": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE "
-                           "(separate passes) -- python3 tools/legs.py cfg2 --steps 5",
+                           f"(separate passes) -- python3 tools/legs.py {leg} --steps 5",
+                           "algorithmic_bytes_per_launch": alg,
+                           "traffic_over_algorithmic": (fetch_b + write_b) / alg,
                            "fetch_size_kb_raw": pmc.get("FETCH_SIZE"), "write_size_kb": pmc.get("WRITE_SIZE"),
                            "correction": "FETCH_SIZE doubled (MI355X_MICROARCH.md: gfx950 counts half of a "
                                          "16-B/lane streaming read)",

@@ -214,6 +214,26 @@ def _prepare(segment: dict, dictionary, lang: str):
     segment["sentence_spans"] = _sentence_spans(text)
 
 
+def _has_alignable(text: str, dictionary, lang: str) -> bool:
+    """Whether _prepare would keep any char of `text` (a non-empty clean_char, alignment.py:
+    137-151): the same stripped range, lower-casing and space -> '|' rule, without building the
+    lists.  align() queues a segment's forward only then, as the reference runs the model only
+    for segments it does not skip (alignment.py:199-202)."""
+    spaces = lang not in LANGUAGES_WITHOUT_SPACES
+    for ch in text.strip():
+        c = ch.lower()
+        if spaces:
+            c = c.replace(" ", "|")
+        if c in dictionary:
+            return True
+    return False
+
+
+class _PackedUnsupported(Exception):
+    """The packed encoder cannot run this model (its frame geometry is not n_frames'): align()
+    redoes the emissions on the per-segment route with the model prepared."""
+
+
 def _logits(model, model_type, waveform_segment, device):
     """alignment.py:217-232 on the device: the [1, T, V] logits of one unpadded forward."""
     if waveform_segment.shape[-1] < 400:
@@ -286,7 +306,8 @@ def _vocab_size(model, model_type):
 _EMISSION_STREAMS = {}
 
 
-def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.environ.get("WX_EMISSION_STREAMS", "8"))):
+def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.environ.get("WX_EMISSION_STREAMS", "8")),
+               allow_packed: bool = True):
     """Emissions of every segment, one unpadded forward each (padding would change wav2vec2's
     logits, alignment.py:217-233), issued round-robin on `n_streams` (8; A/B on config 3: 2 / 4 / 8 streams 803 / 790 / 755 ms) HIP streams: one 30 s
     forward's GEMMs (1,499 rows) fill a fraction of the GPU, so consecutive segments overlap.
@@ -297,7 +318,7 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
     dev = torch.device(device) if not isinstance(device, torch.device) else device
     if dev.type != "cuda":
         return [_emission(model, model_type, w, device) for w in waveforms]
-    packed = (not os.environ.get("WX_MIOPEN_CONV") and model_type == "huggingface"
+    packed = (allow_packed and not os.environ.get("WX_MIOPEN_CONV") and model_type == "huggingface"
               and emission.packed_supported(model))
     if not os.environ.get("WX_MIOPEN_CONV") and not packed:
         emission.prepare_model(model)
@@ -327,8 +348,12 @@ def _emissions(model, model_type, waveforms, device, n_streams: int = int(os.env
             csr.streams = streams
             return csr
         except ValueError:  # a model whose frame geometry is not n_frames': per-segment path
+            # whatever the packs queued on streams[0] finishes before anything else touches
+            # those rows or the model, and the caller redoes the call on the prepared route
+            main.wait_stream(streams[0])
             for st in streams:
-                st.wait_stream(main)
+                st.wait_stream(streams[0])
+            raise _PackedUnsupported() from None
     bad = False
     csr.events = []
     for i, w in enumerate(waveforms):
@@ -467,7 +492,10 @@ def align(
     wavs = []
     for sdx, segment in enumerate(transcript):
         t1, t2 = segment["start"], segment["end"]
-        if t1 >= MAX_DURATION:
+        # no forward for a segment the reference skips before its model call: past the audio,
+        # or no alignable char (music, a script the model lacks: a long one would otherwise pay
+        # a full wav2vec2 forward the reference never runs)
+        if t1 >= MAX_DURATION or not _has_alignable(segment["text"], model_dictionary, model_lang):
             continue
         fwd_pos[sdx] = len(wavs)
         wavs.append(audio[:, int(t1 * SAMPLE_RATE): int(t2 * SAMPLE_RATE)])
@@ -477,9 +505,15 @@ def align(
     # the packed encoder runs the model from its weights: no forward is patched, so the model
     # is not prepared (prepare + restore cost ~5 ms of host time per call before the first kernel)
     packed = gpu_route and model_type == "huggingface" and emission.packed_supported(model)
-    with emission.prepared(model) if gpu_route and not packed else contextlib.nullcontext():
+    with contextlib.ExitStack() as model_ctx:
+        if gpu_route and not packed:
+            model_ctx.enter_context(emission.prepared(model))
         with _Phase("emission"):
-            ems = _emissions(model, model_type, wavs, device)
+            try:
+                ems = _emissions(model, model_type, wavs, device)
+            except _PackedUnsupported:  # per-segment route, model prepared for this call
+                model_ctx.enter_context(emission.prepared(model))
+                ems = _emissions(model, model_type, wavs, device, allow_packed=False)
 
         # 1. text preparation (mutates the input segments like the reference)
         total_segments = len(transcript)

@@ -319,7 +319,9 @@ _LSTM_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 def _lstm_weights(lstm: torch.nn.LSTM, layer: int):
     """(W_ih of both directions [8H, in], b_ih + b_hh [8H], weight_hh [2, 4H, H]) of one layer,
     cached per module until a parameter changes."""
-    key = (layer,) + tuple((p.data_ptr(), p._version) for p in lstm.parameters())
+    # (an inference tensor — a model built or loaded under torch.inference_mode() — has no
+    # version counter: -1, as emission._version)
+    key = (layer,) + tuple((p.data_ptr(), -1 if p.is_inference() else p._version) for p in lstm.parameters())
     c = _LSTM_CACHE.get(lstm)
     if c is None or c[0][1:] != key[1:]:
         c = (key, {})
