@@ -538,6 +538,150 @@ __global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2)))
     }
 }
 
+// The packed launch's one-wave-per-tile form, software-pipelined over key tiles (round 6):
+// while the softmax of key tile k runs on the VALU, the same wave's S^T = K Q^T MFMA chain of
+// tile k + 1 runs on the matrix pipe (two S accumulators, the idiom of cdna_hip_programming.md
+// T15), then tile k's P^T V MFMAs.  The loop body has no branch (a branch ends the block the
+// scheduler interleaves within): the last tile's keys past T are masked by a compare against
+// the uniform count of valid keys, the O rescale is unconditional, loads of tiles past the end
+// are clamped re-reads, and the loop runs over tile pairs with named register sets (A / B) so
+// that nothing is copied between iterations.  Same arithmetic as attn_f32_kernel<1, true>:
+// same MFMA order per accumulator, the same online-softmax updates (bit-identical outputs,
+// tested).  A/B (12 packed 30 s segments, H = 12): 837 -> 819 us per call; forcing the
+// interleave with sched_group_barrier (1 MFMA : 3 or 6 VALU) was slower (1,003 / 959 us).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void attn_f32_pipe_kernel(AttnArgs a) {
+    const unsigned w = [] {
+        const unsigned L = blockIdx.x, n = gridDim.x, x = L % 8, i = L / 8, q = n / 8, r = n % 8;
+        return x * q + min(x, r) + i;
+    }();
+    int lo = 0, hi = a.nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((unsigned)a.seg_units[mid] <= w) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t row0 = a.seg_rows[lo];
+    const int T = a.seg_rows[lo + 1] - (int)row0;
+    const int nq = (T + 31) / 32;
+    const int u = (int)w - a.seg_units[lo];
+    const int tile = u % nq, h = u / nq;
+    const float* Q = a.q + row0 * a.sqt + h * a.sqh;
+    const float* K = a.k + row0 * a.skt + h * a.skh;
+    const float* V = a.v + row0 * a.svt + h * a.svh;
+    const int q0 = tile * 32;
+    const int l = threadIdx.x & 63, r = l & 31, hf = l >> 5;
+    float qv[32];
+    {
+        const float4* qp = reinterpret_cast<const float4*>(Q + (int64_t)min(q0 + r, T - 1) * a.sqt + 32 * hf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = qp[i];
+            qv[4 * i] = x.x;
+            qv[4 * i + 1] = x.y;
+            qv[4 * i + 2] = x.z;
+            qv[4 * i + 3] = x.w;
+        }
+    }
+    const int nk = (T + 31) / 32;  // key tiles
+    f32x16 o0, o1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
+    float m = -INFINITY, lsum = 0.f;
+    float kv[32];                          // K of the next S chain: K[key r][32 hf + j]
+    float va[16], vb[16], wa[16], wb[16];  // V of tiles k (A) and k + 1 (B): V[key(j)][r], V[key(j)][32 + r]
+    auto load_k = [&](int kt) {
+        const int k0 = 32 * min(kt, nk - 1);
+        const float4* kp = reinterpret_cast<const float4*>(K + (int64_t)min(k0 + r, T - 1) * a.skt + 32 * hf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 x = kp[i];
+            kv[4 * i] = x.x;
+            kv[4 * i + 1] = x.y;
+            kv[4 * i + 2] = x.z;
+            kv[4 * i + 3] = x.w;
+        }
+    };
+    auto load_v = [&](int kt, float(&x0)[16], float(&x1)[16]) {
+        const int k0 = 32 * min(kt, nk - 1);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float* vr = V + (int64_t)min(k0 + (j & 3) + 8 * (j >> 2) + 4 * hf, T - 1) * a.svt;
+            x0[j] = vr[r];
+            x1[j] = vr[32 + r];
+        }
+    };
+    auto qk = [&](f32x16& s) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qv[j], s, 0, 0, 0);
+    };
+    // online softmax of tile kt's scores s (in place: s becomes P^T), then O^T += V^T P^T
+    auto softmax_pv = [&](f32x16& s, int kt, const float(&x0)[16], const float(&x1)[16]) {
+        const int valid = T - 32 * kt;  // keys of this tile inside the segment (>= 32: all)
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float x = ((i & 3) + 8 * (i >> 2) + 4 * hf) < valid ? s[i] * a.scale_log2 : -INFINITY;
+            s[i] = x;
+            mx = fmaxf(mx, x);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        float ps = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(s[i] - mn);
+            s[i] = p;
+            ps += p;
+        }
+        ps += __shfl_xor(ps, 32);
+        lsum = lsum * alpha + ps;
+        m = mn;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            o0[i] *= alpha;
+            o1[i] *= alpha;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[j], s[j], o0, 0, 0, 0);
+            o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[j], s[j], o1, 0, 0, 0);
+        }
+    };
+    f32x16 sa, sb;
+    load_k(0);
+    load_v(0, va, vb);
+    qk(sa);  // S of tile 0
+    load_k(1);
+    load_v(1, wa, wb);
+    // tile pairs (kt, kt + 1): S(kt) in sa, V(kt) in va / vb, K(kt + 1) in kv, V(kt + 1) in wa / wb
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {
+        qk(sb);  // S(kt + 1), beside the softmax of tile kt
+        load_k(kt + 2);
+        softmax_pv(sa, kt, va, vb);
+        load_v(kt + 2, va, vb);
+        qk(sa);  // S(kt + 2) (past the end: a clamped re-read, unused)
+        load_k(kt + 3);
+        softmax_pv(sb, kt + 1, wa, wb);
+        load_v(kt + 3, wa, wb);
+    }
+    if (kt < nk) softmax_pv(sa, kt, va, vb);  // an odd count's last tile
+    if (q0 + r >= T) return;
+    const float inv = 1.0f / lsum;
+    float* orow = a.o + ((row0 + q0 + r) * a.H + h) * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // registers 4g..4g+3: head dims 8g + 4hf + 0..3
+        const int d = 8 * g + 4 * hf;
+        *reinterpret_cast<float4*>(orow + d) =
+            make_float4(o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
+        *reinterpret_cast<float4*>(orow + 32 + d) =
+            make_float4(o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    }
+}
+
 // Residual add + LayerNorm over rows of D floats (the wav2vec2 encoder layer's
 // `layer_norm(residual + x)`, twice per layer): one wave per row, the row in registers (D / 256
 // float4 per lane), mean and biased variance in fp32 from the registers (two passes, not
@@ -828,6 +972,11 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     return e == hipSuccess ? WX_OK : (int)e;
 }
 
+static bool attn_pipe() {  // (A/B: WX_ATTN_PIPE=0 runs the unpipelined one-wave kernel)
+    const char* e = getenv("WX_ATTN_PIPE");
+    return !(e && e[0] == '0');
+}
+
 extern "C" int wx_attention_f32_packed(const float* q, const float* k, const float* v, float* o, int32_t nseg,
                                        const int32_t* seg_rows, const int32_t* seg_units, int32_t n_units,
                                        int32_t H, int32_t D, const int64_t* q_strides, const int64_t* k_strides,
@@ -868,7 +1017,12 @@ extern "C" int wx_attention_f32_packed(const float* q, const float* k, const flo
     // with ~10 units per CU or more, one wave per tile (no merge) keeps them as busy
     if (split <= 0) split = n_units >= 2560 ? 1 : 4;
     switch (split) {
-        case 1: hipLaunchKernelGGL((attn_f32_kernel<1, true>), dim3((unsigned)n_units), dim3(64), 0, s, a); break;
+        case 1:
+            if (attn_pipe())
+                hipLaunchKernelGGL(attn_f32_pipe_kernel, dim3((unsigned)n_units), dim3(64), 0, s, a);
+            else
+                hipLaunchKernelGGL((attn_f32_kernel<1, true>), dim3((unsigned)n_units), dim3(64), 0, s, a);
+            break;
         case 2: hipLaunchKernelGGL((attn_f32_kernel<2, true>), dim3((unsigned)n_units), dim3(128), 0, s, a); break;
         case 4: hipLaunchKernelGGL((attn_f32_kernel<4, true>), dim3((unsigned)n_units), dim3(256), 0, s, a); break;
         default: return WX_E_INVALID;
