@@ -224,11 +224,16 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
 // per hour of audio, ~29% of the producer's GPU time).  Here the input projection of every
 // step (x W_ih^T + b_ih + b_hh, both directions) is one GEMM before the call (xp), and one
 // workgroup carries 16 sequences of one direction through all T steps: per step
-//   gates[16, 512] = xp[t] + h_{t-1} W_hh^T     (v_mfma_f32_16x16x4_f32: wave w computes gate
-//                                               w's 128 columns, W_hh's fragments held in
-//                                               registers for the whole sequence)
-//   i, f, o = sigmoid, g = tanh -> LDS;  c = f c + i g;  h = o tanh(c) -> LDS (next step's A
-//   operand) and y[b, t, d H + u].
+//   gates[16, 512] = xp[t] + h_{t-1} W_hh^T     (v_mfma_f32_16x16x4_f32, W_hh's fragments held
+//                                               in registers for the whole sequence)
+//   i, f, o = sigmoid, g = tanh;  c = f c + i g;  h = o tanh(c) -> LDS (next step's A operand)
+//   and y[b, t, d H + u].
+// Round 6: wave w owns hidden units 32 w .. 32 w + 31 across all four gates (tiles 2 g + half:
+// gate g's columns 128 g + 32 w + 16 half + 0..15), so a lane holds i, f, g, o of the same
+// (sequence, unit) in its own accumulators and the cell update is lane-local: one barrier per
+// step (h into a ping-pong LDS buffer) instead of the gate activations' LDS round trip and two
+// barriers (round 5: wave w computed gate w for all units).  Same MFMA order per gate value and
+// the same activation functions as before: bit-identical outputs.
 // fp32 throughout (fma chains in the MFMA, not bit-identical to MIOpen's; tests compare with
 // torch.nn.LSTM at fp32 tolerance).  H = 128 (PyanNet).
 constexpr int kLH = 128;  // hidden size
@@ -241,43 +246,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float* __restrict__ y /* [B][T][2H] */, int B, int T) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     constexpr int RS = kLH + 4;  // h row stride in LDS (floats)
-    __shared__ __attribute__((aligned(16))) float hs[kLR * RS];
-    __shared__ __attribute__((aligned(16))) float gs[4][kLR][kLH];
+    __shared__ __attribute__((aligned(16))) float hs[2][kLR * RS];  // ping-pong by step parity
     const int d = blockIdx.y;
     const int b0 = blockIdx.x * kLR;
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
-    // this wave's W_hh fragments, kept for the whole sequence: gate w's rows n = 128 w + 16 tile + r16,
-    // k = 16 kk + 4 q .. + 3
+    // gate column of tile tt = 2 g + half: 128 g + 32 w + 16 half + r16
+    auto col = [&](int tt) { return 128 * (tt >> 1) + 32 * w + 16 * (tt & 1) + r16; };
+    // this wave's W_hh fragments, kept for the whole sequence: rows col(tile), k = 16 kk + 4 q .. + 3
     const float* wd = whh + (int64_t)d * 4 * kLH * kLH;
     float4 wf[8][8];  // [tile][kk]
 #pragma unroll
     for (int tile = 0; tile < 8; ++tile)
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
-            wf[tile][kk] = *reinterpret_cast<const float4*>(wd + (int64_t)(128 * w + 16 * tile + r16) * kLH + 16 * kk + 4 * q);
-    for (int i = threadIdx.x; i < kLR * RS; i += 256) hs[i] = 0.f;
-    // cell state: thread owns row e / H, units (e % H) .. +7 for e = 8 threadIdx
-    const int er = (threadIdx.x * 8) / kLH, eu = (threadIdx.x * 8) % kLH;
-    float c[8];
+            wf[tile][kk] = *reinterpret_cast<const float4*>(wd + (int64_t)col(tile) * kLH + 16 * kk + 4 * q);
+    for (int i = threadIdx.x; i < kLR * RS; i += 256) hs[0][i] = 0.f;
+    // cell state of (sequence 4 q + v, unit 32 w + 16 half + r16): c[half][v]
+    float c[2][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] = 0.f;
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) c[i][v] = 0.f;
     __syncthreads();
-    // xp rows of a step: accumulator (tile, v) <-> row 4 q + v, column 16 tile + r16 of gate w;
-    // the next step's are loaded while this step's MFMAs run
+    // xp of a step: accumulator (tile, v) <-> sequence 4 q + v, column col(tile); the next step's
+    // are loaded while this step's MFMAs run
     float xn[8][4];
     auto load_xp = [&](int s) {
         const int t = d ? T - 1 - s : s;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const int b = min(b0 + 4 * q + v, B - 1);
-            const float* xr = xp + (((int64_t)b * T + t) * 2 + d) * 4 * kLH + 128 * w + r16;
+            const float* xr = xp + (((int64_t)b * T + t) * 2 + d) * 4 * kLH;
 #pragma unroll
-            for (int tile = 0; tile < 8; ++tile) xn[tile][v] = xr[16 * tile];
+            for (int tile = 0; tile < 8; ++tile) xn[tile][v] = xr[col(tile)];
         }
     };
     load_xp(0);
     for (int s = 0; s < T; ++s) {
         const int t = d ? T - 1 - s : s;
+        const float* hr = hs[s & 1];
+        float* hw = hs[(s + 1) & 1];
         f32x4 acc[8];
 #pragma unroll
         for (int tile = 0; tile < 8; ++tile)
@@ -286,7 +294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (s + 1 < T) load_xp(s + 1);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
-            const float4 a = *reinterpret_cast<const float4*>(hs + r16 * RS + 16 * kk + 4 * q);
+            const float4 a = *reinterpret_cast<const float4*>(hr + r16 * RS + 16 * kk + 4 * q);
 #pragma unroll
             for (int tile = 0; tile < 8; ++tile) {
                 acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wf[tile][kk].x, acc[tile], 0, 0, 0);
@@ -295,31 +303,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 acc[tile] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wf[tile][kk].w, acc[tile], 0, 0, 0);
             }
         }
-        // gate activations (PyTorch order i, f, g, o: wave 2 is the tanh gate)
+        // gates (PyTorch order i, f, g, o) and the cell update, lane-local
 #pragma unroll
-        for (int tile = 0; tile < 8; ++tile)
+        for (int half = 0; half < 2; ++half) {
+            const int u = 32 * w + 16 * half + r16;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
-                const float x = acc[tile][v];
-                gs[w][4 * q + v][16 * tile + r16] = w == 2 ? tanhf(x) : sigmoid_f(x);
+                const float ig = sigmoid_f(acc[half][v]), fg = sigmoid_f(acc[2 + half][v]);
+                const float gg = tanhf(acc[4 + half][v]), og = sigmoid_f(acc[6 + half][v]);
+                c[half][v] = fg * c[half][v] + ig * gg;
+                const float h = og * tanhf(c[half][v]);
+                hw[(4 * q + v) * RS + u] = h;
+                const int b = b0 + 4 * q + v;
+                if (b < B) y[((int64_t)b * T + t) * 2 * kLH + d * kLH + u] = h;
             }
-        __syncthreads();
-        float hv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int u = eu + i;
-            const float ig = gs[0][er][u], fg = gs[1][er][u], gg = gs[2][er][u], og = gs[3][er][u];
-            c[i] = fg * c[i] + ig * gg;
-            hv[i] = og * tanhf(c[i]);
         }
-        *reinterpret_cast<float4*>(hs + er * RS + eu) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-        *reinterpret_cast<float4*>(hs + er * RS + eu + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
-        if (b0 + er < B) {
-            float* yr = y + ((int64_t)(b0 + er) * T + t) * 2 * kLH + d * kLH + eu;
-            *reinterpret_cast<float4*>(yr) = make_float4(hv[0], hv[1], hv[2], hv[3]);
-            *reinterpret_cast<float4*>(yr + 4) = make_float4(hv[4], hv[5], hv[6], hv[7]);
-        }
-        __syncthreads();
+        __syncthreads();  // h_t complete in hw before any wave reads it as the next A operand
     }
 }
 
