@@ -130,6 +130,13 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
 // outputs (60 used) on v_mfma_f32_16x16x4_f32; + bias, written once.  fp32 (fma chains: not
 // bit-identical to the GEMM route, tests compare at fp32 tolerance).
 constexpr int kCkFrames = 128;
+#ifndef WX_DEV_CK_WBUFS
+#define WX_DEV_CK_WBUFS 1
+#endif
+// weight slabs in LDS: one (round 6) keeps a block at 64 KB (Cin 80), so two blocks share a CU
+// and one's weight load / barriers hide under the other's MFMAs; two (round 5: 84 KB, one block
+// per CU) overlapped the next tap's slab store with the current tap inside the block
+constexpr int kCkWBufs = WX_DEV_CK_WBUFS;
 
 template <int CINP, int KT>
 __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict__ x, int Cin, int L,
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
     constexpr int NB4 = CINP * 64 / 4;
     constexpr int PER = (NB4 + 255) / 256;
     __shared__ __attribute__((aligned(16))) float xa[WR * RS];
-    __shared__ __attribute__((aligned(16))) float wb[2][CINP * 64];
+    __shared__ __attribute__((aligned(16))) float wb[kCkWBufs][CINP * 64];
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * kCkFrames;
     const float* xb = x + (int64_t)b * L * Cin;
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
         if (j + 1 < KT) {
             WX_CT_BLOAD(j + 1)
         }
-        const float* bb = wb[j & 1] + (q * 64 + r16) * 4;
+        const float* bb = wb[kCkWBufs == 2 ? (j & 1) : 0] + (q * 64 + r16) * 4;
 #pragma unroll
         for (int ic = 0; ic < NIC; ++ic) {
             float4 av[2], bv[NOB];
@@ -195,10 +202,18 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
                     acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].w, bv[ob].w, acc[fb][ob], 0, 0, 0);
                 }
         }
-        if (j + 1 < KT) {
-            WX_CT_BSTORE((j + 1) & 1)
+        if constexpr (kCkWBufs == 2) {
+            if (j + 1 < KT) {
+                WX_CT_BSTORE((j + 1) & 1)
+            }
+            __syncthreads();
+        } else {
+            __syncthreads();  // every wave is done with tap j's slab
+            if (j + 1 < KT) {
+                WX_CT_BSTORE(0)
+                __syncthreads();
+            }
         }
-        __syncthreads();
     }
 #undef WX_CT_BLOAD
 #undef WX_CT_BSTORE
