@@ -50,6 +50,11 @@ case $MODE in
     stats_leg "$RND" e2e || exit 1
     stats_leg "$RND" e2e5 || exit 1
     cd "$R" && python3 tools/summarize_profiles.py "$RND" > "gpurun_out/summarize_$RND.log" 2>&1 || { echo "summarize failed"; tail -20 "gpurun_out/summarize_$RND.log"; exit 1; }
+    # per-kernel rooflines of the producers from the same kernel traces
+    T_VAD=$(find "gpurun_out/prof_$RND/vad1h/stats" -name "*kernel_trace.csv" | head -1)
+    [ -n "$T_VAD" ] && python3 tools/vad_roofline.py "$T_VAD" --out "profiles/${RND}_vad_roofline.json" > /dev/null
+    T_E2E=$(find "gpurun_out/prof_$RND/e2e/stats" -name "*kernel_trace.csv" | head -1)
+    [ -n "$T_E2E" ] && python3 tools/forward_roofline.py "$T_E2E" --out "profiles/${RND}_forward_roofline.json" > /dev/null
     mkdir -p "gpurun_out/profiles_$RND" && cp profiles/${RND}_* "gpurun_out/profiles_$RND/"
     for LEG in vad1h e2e e2e5; do
       find "gpurun_out/prof_$RND/$LEG/stats" -name "*kernel_stats.csv" -exec cp {} "gpurun_out/profiles_$RND/${RND}_${LEG}_kernel_stats.csv" \;
