@@ -126,17 +126,14 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
 // GEMMs (vad_model.conv1d_batched) each was 5 passes over the [B L, Cin] activation with the
 // [B L, 60] output read and written per tap (memory-bound, ~33 ms per hour of audio).  Here
 // one block per (window, 128 output frames): the 132 input rows sit in LDS once, the taps'
-// [Cin, 64] weight slabs stream through a double-buffered LDS slab, 4 waves x 32 frames x 64
+// [Cin, 64] weight slabs stream through one LDS slab, 4 waves x 32 frames x 64
 // outputs (60 used) on v_mfma_f32_16x16x4_f32; + bias, written once.  fp32 (fma chains: not
 // bit-identical to the GEMM route, tests compare at fp32 tolerance).
 constexpr int kCkFrames = 128;
-#ifndef WX_DEV_CK_WBUFS
-#define WX_DEV_CK_WBUFS 1
-#endif
-// weight slabs in LDS: one (round 6) keeps a block at 64 KB (Cin 80), so two blocks share a CU
-// and one's weight load / barriers hide under the other's MFMAs; two (round 5: 84 KB, one block
-// per CU) overlapped the next tap's slab store with the current tap inside the block
-constexpr int kCkWBufs = WX_DEV_CK_WBUFS;
+// One weight slab in LDS (round 6): a block is 64 KB (Cin 80), so two blocks share a CU and
+// one's slab load and barriers hide under the other's MFMAs.  (Round 5 double-buffered the slab
+// — 84 KB, one block per CU, the next tap's store overlapped inside the block: 1 ms per hour
+// slower.)
 
 template <int CINP, int KT>
 __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict__ x, int Cin, int L,
@@ -150,7 +147,7 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
     constexpr int NB4 = CINP * 64 / 4;
     constexpr int PER = (NB4 + 255) / 256;
     __shared__ __attribute__((aligned(16))) float xa[WR * RS];
-    __shared__ __attribute__((aligned(16))) float wb[kCkWBufs][CINP * 64];
+    __shared__ __attribute__((aligned(16))) float wb[CINP * 64];
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * kCkFrames;
     const float* xb = x + (int64_t)b * L * Cin;
@@ -166,11 +163,11 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
     float4 breg[PER];
 #define WX_CT_BLOAD(j) \
     _Pragma("unroll") for (int p = 0; p < PER; ++p) breg[p] = wg[(int64_t)(j) * NB4 + min((int)threadIdx.x + 256 * p, NB4 - 1)];
-#define WX_CT_BSTORE(buf)                                                                 \
+#define WX_CT_BSTORE()                                                                    \
     _Pragma("unroll") for (int p = 0; p < PER; ++p) if ((int)threadIdx.x + 256 * p < NB4) \
-        reinterpret_cast<float4*>(wb[buf])[threadIdx.x + 256 * p] = breg[p];
+        reinterpret_cast<float4*>(wb)[threadIdx.x + 256 * p] = breg[p];
     WX_CT_BLOAD(0)
-    WX_CT_BSTORE(0)
+    WX_CT_BSTORE()
     __syncthreads();
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
     f32x4 acc[2][NOB];
@@ -184,7 +181,7 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
         if (j + 1 < KT) {
             WX_CT_BLOAD(j + 1)
         }
-        const float* bb = wb[kCkWBufs == 2 ? (j & 1) : 0] + (q * 64 + r16) * 4;
+        const float* bb = wb + (q * 64 + r16) * 4;
 #pragma unroll
         for (int ic = 0; ic < NIC; ++ic) {
             float4 av[2], bv[NOB];
@@ -202,17 +199,10 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
                     acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].w, bv[ob].w, acc[fb][ob], 0, 0, 0);
                 }
         }
-        if constexpr (kCkWBufs == 2) {
-            if (j + 1 < KT) {
-                WX_CT_BSTORE((j + 1) & 1)
-            }
+        __syncthreads();  // every wave is done with tap j's slab
+        if (j + 1 < KT) {
+            WX_CT_BSTORE()
             __syncthreads();
-        } else {
-            __syncthreads();  // every wave is done with tap j's slab
-            if (j + 1 < KT) {
-                WX_CT_BSTORE(0)
-                __syncthreads();
-            }
         }
     }
 #undef WX_CT_BLOAD
