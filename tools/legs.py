@@ -34,7 +34,7 @@ def main():
         from whisperx_amd.vad_model import VoiceActivitySegmentation
 
         torch.manual_seed(5)
-        vad = VoiceActivitySegmentation(device=dev, batch_size=2048)
+        vad = VoiceActivitySegmentation(device=dev, batch_size=int(os.environ.get("WX_VAD_BATCH", "2048")))
         wav = (torch.randn(1, 3600 * 16000, generator=torch.Generator().manual_seed(5)) * 0.1).to(dev)
         vad({"waveform": wav, "sample_rate": 16000})
         torch.cuda.synchronize()
