@@ -476,3 +476,55 @@ def test_align_leaves_callers_model_unchanged():
     assert sd0.keys() == sd1.keys() and all(torch.equal(sd0[k], sd1[k]) for k in sd0)
     with torch.inference_mode():
         assert torch.equal(m(x).logits, y0)
+
+
+@pytest.mark.gpu
+def test_align_packed_value_error_redoes_call_on_prepared_route(monkeypatch):
+    """When emission.packed_logits raises ValueError (a frame geometry n_frames does not
+    predict), align() joins what the packs queued, enters emission.prepared() and redoes the
+    emissions per segment: same words as the packed route (times within one 20 ms frame) and the
+    caller's model unchanged afterwards."""
+    from transformers import Wav2Vec2Config, Wav2Vec2ForCTC
+
+    from whisperx_amd import align, emission
+
+    torch.manual_seed(11)
+    m = Wav2Vec2ForCTC(Wav2Vec2Config(vocab_size=32, num_hidden_layers=2)).cuda().eval()
+    x = (torch.randn(1, 6 * 16000, generator=torch.Generator().manual_seed(12)) * 0.1).cuda()
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    dictionary = {c: i + 4 for i, c in enumerate(letters)}
+    dictionary.update({"<pad>": 0, "|": 1})
+    meta = {"language": "en", "dictionary": dictionary, "type": "huggingface"}
+
+    def segs():
+        return [{"start": 0.0, "end": 2.0, "text": "hello world"},
+                {"start": 2.0, "end": 4.5, "text": "again here"},
+                {"start": 4.5, "end": 6.0, "text": "last one"}]
+
+    assert emission.packed_supported(m)
+    ref = align(segs(), m, meta, x[0], "cuda:0")
+    calls = []
+
+    def refuse(*a, **k):
+        calls.append(1)
+        raise ValueError("frame geometry")
+
+    entered = []
+    prepared = emission.prepared
+
+    def spy(model):
+        entered.append(model)
+        return prepared(model)
+
+    monkeypatch.setattr(emission, "packed_logits", refuse)
+    monkeypatch.setattr(emission, "prepared", spy)
+    got = align(segs(), m, meta, x[0], "cuda:0")
+    assert calls, "the packed route was not taken"
+    assert entered == [m], "the per-segment redo did not run on the prepared model"
+    assert len(got["word_segments"]) == len(ref["word_segments"]) == 6
+    for a, b in zip(got["word_segments"], ref["word_segments"]):
+        assert a["word"] == b["word"]
+        assert abs(a["start"] - b["start"]) <= 0.0201 and abs(a["end"] - b["end"]) <= 0.0201, (a, b)
+    assert not any("forward" in mod.__dict__ or hasattr(mod, "_wx_w_cache") or hasattr(mod, "_wx_orig_forward")
+                   for mod in m.modules())
+    assert not hasattr(m, "_wx_gemm_conv") and not hasattr(m, "_wx_orig_attn")
