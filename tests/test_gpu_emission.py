@@ -131,27 +131,6 @@ def test_attention_f32_packed_vs_fp64(split):
         torch.testing.assert_close(got[:, a:b], ref, rtol=1e-5, atol=2e-5, msg=f"segment rows [{a}, {b})")
 
 
-def test_attention_f32_packed_pipelined_equals_unpipelined(monkeypatch):
-    """The software-pipelined one-wave kernel (attn_f32_pipe_kernel: tile k + 1's S chain beside
-    tile k's softmax) does the same arithmetic in the same order as the one-wave kernel it
-    replaced (WX_ATTN_PIPE=0): bit-identical outputs on ragged packed segments (odd and even key
-    tile counts, partial last tiles)."""
-    from whisperx_amd import _lib
-
-    torch.manual_seed(5)
-    H = 16
-    lengths = [1499, 37, 1, 64, 33, 2999, 96, 95]
-    segs = _lib.PackedSegments(lengths)
-    R = segs.rows
-    qkv = torch.randn(1, R, 3 * H * 64, device="cuda") * 2
-    q, k, v = (qkv[..., i * H * 64:(i + 1) * H * 64].view(1, R, H, 64).transpose(1, 2) for i in range(3))
-    monkeypatch.setenv("WX_ATTN_PIPE", "0")
-    old = _lib.attention_f32_packed(q, k, v, 0.125, segs, 1)
-    monkeypatch.setenv("WX_ATTN_PIPE", "1")
-    new = _lib.attention_f32_packed(q, k, v, 0.125, segs, 1)
-    assert torch.equal(old, new)
-
-
 @pytest.mark.parametrize("D,residual", [(768, True), (768, False), (1024, True)])
 def test_posconv_packed_vs_torch(D, residual):
     """wx_posconv_packed (the positional conv embedding of every packed segment in one launch:

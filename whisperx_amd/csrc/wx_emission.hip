@@ -349,10 +349,16 @@ struct AttnArgs {
 
 constexpr int kAttnSplit = 4;  // waves per 32-query tile, each over every kAttnSplit-th 32-key tile
 
-// amdgpu_waves_per_eu(2): the occupancy it gets anyway (242 registers), stated so the allocator
-// keeps everything in 203 VGPRs instead of splitting 194 / 48 with AGPR copies (A/B: 1-2% faster).
-// A third wave per SIMD (168 registers: V loaded behind the S chain instead of a tile ahead,
-// 2 spills) was 10-15% slower.
+// amdgpu_waves_per_eu(2): two waves per SIMD, stated so the allocator keeps everything in VGPRs
+// (~230 with the buffer-descriptor loads) instead of splitting them with AGPR copies (A/B: 1-2%
+// faster).  A third wave per SIMD (168 registers: V loaded behind the S chain instead of a tile
+// ahead, 2 spills) was 10-15% slower.  Round 6: the K / V loads through per-tile buffer
+// descriptors (no per-lane address arithmetic) and no key compare on whole tiles took 12 packed
+// 30 s segments (H = 12) from 818 to 727 us per call; PMC before the change: 327 VALU
+// instructions per (wave, key tile) beside 64 MFMAs, ~150 of them address arithmetic (32-bit
+// multiplies and 64-bit adds), MFMA busy 65% of the cycles.  With it the software-pipelined
+// one-wave form of the same kernel (tile k + 1's S chain beside tile k's softmax, +2% before)
+// measured equal (729 us) and was removed.
 // SPLIT waves per 32-query tile (each over every SPLIT-th 32-key tile; SPLIT = 1: one wave, no
 // merge); PACKED: one launch over many segments of their own lengths (rows packed back to back)
 template <int SPLIT, bool PACKED>
@@ -416,24 +422,34 @@ __global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
     for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
     float m = -INFINITY, lsum = 0.f;
-    // K / V of the wave's next key tile are loaded while the current one computes
+    // K / V of the wave's next key tile are loaded while the current one computes, through
+    // buffer descriptors rebased per key tile (as attn_f32_pipe_kernel: no per-lane address
+    // arithmetic; keys past the end read zeros, masked like the clamped re-reads they replace)
     float kv[32], va[16], vb[16];  // K[key r][32 hf + j]; V[key(j)][r], V[key(j)][32 + r]
+    const int64_t skt = a.skt, svt = a.svt;
+    const int vk = (int)((r * skt + 32 * hf) * 4), vv = (int)((4 * hf * svt + r) * 4);
+    auto tile_rsrc = [&](const float* base, int64_t stride, int k0) {
+        k0 = __builtin_amdgcn_readfirstlane(k0);  // (32 wv + ...: uniform, which hipcc cannot prove)
+        const int64_t rem = (int64_t)(T - 1 - k0) * stride + 64;
+        const int n = rem <= 0 ? 0 : (int)min(rem * 4, (int64_t)0x7fffffff);
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + (int64_t)k0 * stride), 0, n, 0x00020000);
+    };
     auto load_kv = [&](int k0, float(&kk)[32], float(&a0)[16], float(&a1)[16]) {
-        const float4* kp = reinterpret_cast<const float4*>(K + (int64_t)min(k0 + r, T - 1) * a.skt + 32 * hf);
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rk = tile_rsrc(K, skt, k0), rv = tile_rsrc(V, svt, k0);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const float4 x = kp[i];
-            kk[4 * i] = x.x;
-            kk[4 * i + 1] = x.y;
-            kk[4 * i + 2] = x.z;
-            kk[4 * i + 3] = x.w;
+            const u4 x = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rk, vk + 16 * i, 0, 0));
+            kk[4 * i] = __uint_as_float(x.x);
+            kk[4 * i + 1] = __uint_as_float(x.y);
+            kk[4 * i + 2] = __uint_as_float(x.z);
+            kk[4 * i + 3] = __uint_as_float(x.w);
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const int key = min(k0 + (j & 3) + 8 * (j >> 2) + 4 * hf, T - 1);
-            const float* vr = V + (int64_t)key * a.svt;
-            a0[j] = vr[r];
-            a1[j] = vr[32 + r];
+            const int so = (int)(((j & 3) + 8 * (j >> 2)) * svt * 4);
+            a0[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, vv, so, 0));
+            a1[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, vv + 128, so, 0));
         }
     };
     if (32 * wv < T) load_kv(32 * wv, kv, va, vb);
@@ -444,17 +460,22 @@ __global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
         for (int j = 0; j < 32; ++j) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qv[j], s, 0, 0, 0);
         float van[16], vbn[16];
-        {
-            const int kn = min(k0 + 32 * SPLIT, T - 1);  // (past the end: a harmless re-read)
-            load_kv(kn, kv, van, vbn);  // kv is dead once the S chain has been issued
-        }
+        load_kv(k0 + 32 * SPLIT, kv, van, vbn);  // (past the end: zeros, unused); kv is dead once the S chain has been issued
         float mx = -INFINITY;
+        if (k0 + 32 <= T) {  // a whole key tile: no key compare (uniform branch)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-            const float x = key < T ? s[i] * a.scale_log2 : -INFINITY;
-            s[i] = x;
-            mx = fmaxf(mx, x);
+            for (int i = 0; i < 16; ++i) {
+                s[i] = s[i] * a.scale_log2;
+                mx = fmaxf(mx, s[i]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key = k0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                const float x = key < T ? s[i] * a.scale_log2 : -INFINITY;
+                s[i] = x;
+                mx = fmaxf(mx, x);
+            }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 32));
         const float mn = fmaxf(m, mx);
@@ -525,150 +546,6 @@ __global__ __launch_bounds__(64 * SPLIT) __attribute__((amdgpu_waves_per_eu(2)))
         }
     }
     }
-    if (q0 + r >= T) return;
-    const float inv = 1.0f / lsum;
-    float* orow = a.o + ((row0 + q0 + r) * a.H + h) * 64;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // registers 4g..4g+3: head dims 8g + 4hf + 0..3
-        const int d = 8 * g + 4 * hf;
-        *reinterpret_cast<float4*>(orow + d) =
-            make_float4(o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-        *reinterpret_cast<float4*>(orow + 32 + d) =
-            make_float4(o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-    }
-}
-
-// The packed launch's one-wave-per-tile form, software-pipelined over key tiles (round 6):
-// while the softmax of key tile k runs on the VALU, the same wave's S^T = K Q^T MFMA chain of
-// tile k + 1 runs on the matrix pipe (two S accumulators, the idiom of cdna_hip_programming.md
-// T15), then tile k's P^T V MFMAs.  The loop body has no branch (a branch ends the block the
-// scheduler interleaves within): the last tile's keys past T are masked by a compare against
-// the uniform count of valid keys, the O rescale is unconditional, loads of tiles past the end
-// are clamped re-reads, and the loop runs over tile pairs with named register sets (A / B) so
-// that nothing is copied between iterations.  Same arithmetic as attn_f32_kernel<1, true>:
-// same MFMA order per accumulator, the same online-softmax updates (bit-identical outputs,
-// tested).  A/B (12 packed 30 s segments, H = 12): 837 -> 819 us per call; forcing the
-// interleave with sched_group_barrier (1 MFMA : 3 or 6 VALU) was slower (1,003 / 959 us).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void attn_f32_pipe_kernel(AttnArgs a) {
-    const unsigned w = [] {
-        const unsigned L = blockIdx.x, n = gridDim.x, x = L % 8, i = L / 8, q = n / 8, r = n % 8;
-        return x * q + min(x, r) + i;
-    }();
-    int lo = 0, hi = a.nseg - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((unsigned)a.seg_units[mid] <= w) lo = mid;
-        else hi = mid - 1;
-    }
-    const int64_t row0 = a.seg_rows[lo];
-    const int T = a.seg_rows[lo + 1] - (int)row0;
-    const int nq = (T + 31) / 32;
-    const int u = (int)w - a.seg_units[lo];
-    const int tile = u % nq, h = u / nq;
-    const float* Q = a.q + row0 * a.sqt + h * a.sqh;
-    const float* K = a.k + row0 * a.skt + h * a.skh;
-    const float* V = a.v + row0 * a.svt + h * a.svh;
-    const int q0 = tile * 32;
-    const int l = threadIdx.x & 63, r = l & 31, hf = l >> 5;
-    float qv[32];
-    {
-        const float4* qp = reinterpret_cast<const float4*>(Q + (int64_t)min(q0 + r, T - 1) * a.sqt + 32 * hf);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 x = qp[i];
-            qv[4 * i] = x.x;
-            qv[4 * i + 1] = x.y;
-            qv[4 * i + 2] = x.z;
-            qv[4 * i + 3] = x.w;
-        }
-    }
-    const int nk = (T + 31) / 32;  // key tiles
-    f32x16 o0, o1;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o0[i] = o1[i] = 0.f;
-    float m = -INFINITY, lsum = 0.f;
-    float kv[32];                          // K of the next S chain: K[key r][32 hf + j]
-    float va[16], vb[16], wa[16], wb[16];  // V of tiles k (A) and k + 1 (B): V[key(j)][r], V[key(j)][32 + r]
-    auto load_k = [&](int kt) {
-        const int k0 = 32 * min(kt, nk - 1);
-        const float4* kp = reinterpret_cast<const float4*>(K + (int64_t)min(k0 + r, T - 1) * a.skt + 32 * hf);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 x = kp[i];
-            kv[4 * i] = x.x;
-            kv[4 * i + 1] = x.y;
-            kv[4 * i + 2] = x.z;
-            kv[4 * i + 3] = x.w;
-        }
-    };
-    auto load_v = [&](int kt, float(&x0)[16], float(&x1)[16]) {
-        const int k0 = 32 * min(kt, nk - 1);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float* vr = V + (int64_t)min(k0 + (j & 3) + 8 * (j >> 2) + 4 * hf, T - 1) * a.svt;
-            x0[j] = vr[r];
-            x1[j] = vr[32 + r];
-        }
-    };
-    auto qk = [&](f32x16& s) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[j], qv[j], s, 0, 0, 0);
-    };
-    // online softmax of tile kt's scores s (in place: s becomes P^T), then O^T += V^T P^T
-    auto softmax_pv = [&](f32x16& s, int kt, const float(&x0)[16], const float(&x1)[16]) {
-        const int valid = T - 32 * kt;  // keys of this tile inside the segment (>= 32: all)
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float x = ((i & 3) + 8 * (i >> 2) + 4 * hf) < valid ? s[i] * a.scale_log2 : -INFINITY;
-            s[i] = x;
-            mx = fmaxf(mx, x);
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mn = fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        float ps = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float p = __builtin_amdgcn_exp2f(s[i] - mn);
-            s[i] = p;
-            ps += p;
-        }
-        ps += __shfl_xor(ps, 32);
-        lsum = lsum * alpha + ps;
-        m = mn;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            o0[i] *= alpha;
-            o1[i] *= alpha;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0[j], s[j], o0, 0, 0, 0);
-            o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1[j], s[j], o1, 0, 0, 0);
-        }
-    };
-    f32x16 sa, sb;
-    load_k(0);
-    load_v(0, va, vb);
-    qk(sa);  // S of tile 0
-    load_k(1);
-    load_v(1, wa, wb);
-    // tile pairs (kt, kt + 1): S(kt) in sa, V(kt) in va / vb, K(kt + 1) in kv, V(kt + 1) in wa / wb
-    int kt = 0;
-    for (; kt + 2 <= nk; kt += 2) {
-        qk(sb);  // S(kt + 1), beside the softmax of tile kt
-        load_k(kt + 2);
-        softmax_pv(sa, kt, va, vb);
-        load_v(kt + 2, va, vb);
-        qk(sa);  // S(kt + 2) (past the end: a clamped re-read, unused)
-        load_k(kt + 3);
-        softmax_pv(sb, kt + 1, wa, wb);
-        load_v(kt + 3, wa, wb);
-    }
-    if (kt < nk) softmax_pv(sa, kt, va, vb);  // an odd count's last tile
     if (q0 + r >= T) return;
     const float inv = 1.0f / lsum;
     float* orow = a.o + ((row0 + q0 + r) * a.H + h) * 64;
@@ -972,10 +849,6 @@ extern "C" int wx_attention_f32(const float* q, const float* k, const float* v, 
     return e == hipSuccess ? WX_OK : (int)e;
 }
 
-static bool attn_pipe() {  // (A/B: WX_ATTN_PIPE=0 runs the unpipelined one-wave kernel)
-    const char* e = getenv("WX_ATTN_PIPE");
-    return !(e && e[0] == '0');
-}
 
 extern "C" int wx_attention_f32_packed(const float* q, const float* k, const float* v, float* o, int32_t nseg,
                                        const int32_t* seg_rows, const int32_t* seg_units, int32_t n_units,
@@ -1017,12 +890,7 @@ extern "C" int wx_attention_f32_packed(const float* q, const float* k, const flo
     // with ~10 units per CU or more, one wave per tile (no merge) keeps them as busy
     if (split <= 0) split = n_units >= 2560 ? 1 : 4;
     switch (split) {
-        case 1:
-            if (attn_pipe())
-                hipLaunchKernelGGL(attn_f32_pipe_kernel, dim3((unsigned)n_units), dim3(64), 0, s, a);
-            else
-                hipLaunchKernelGGL((attn_f32_kernel<1, true>), dim3((unsigned)n_units), dim3(64), 0, s, a);
-            break;
+        case 1: hipLaunchKernelGGL((attn_f32_kernel<1, true>), dim3((unsigned)n_units), dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL((attn_f32_kernel<2, true>), dim3((unsigned)n_units), dim3(128), 0, s, a); break;
         case 4: hipLaunchKernelGGL((attn_f32_kernel<4, true>), dim3((unsigned)n_units), dim3(256), 0, s, a); break;
         default: return WX_E_INVALID;
