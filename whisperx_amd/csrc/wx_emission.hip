@@ -665,15 +665,30 @@ __global__ __launch_bounds__(256) void posconv_kernel(PosConvArgs a) {
         *reinterpret_cast<float4*>(xa + r * RS + 4 * c4) = v;
     }
     const float4* wg = reinterpret_cast<const float4*>(a.w) + (int64_t)g * kPcK * NB4;
-    float4 breg[PER];  // (the last slot of a partial tap re-reads a valid element; not stored)
-#define WX_PC_BLOAD(j)                                                                    \
-    _Pragma("unroll") for (int p = 0; p < PER; ++p) breg[p] =                             \
-        wg[(int64_t)(j) * NB4 + min((int)threadIdx.x + 256 * p, NB4 - 1)];
-#define WX_PC_BSTORE(buf)                                                                 \
-    _Pragma("unroll") for (int p = 0; p < PER; ++p) if ((int)threadIdx.x + 256 * p < NB4) \
-        reinterpret_cast<float4*>(wb[buf])[threadIdx.x + 256 * p] = breg[p];
-    WX_PC_BLOAD(0)
-    WX_PC_BSTORE(0)
+    // the next tap's weights in named registers, loaded unconditionally (the last slot of a
+    // partial tap re-reads a valid element, not stored) and pinned above the tap's MFMAs by a
+    // sched_barrier: a register array with conditional stores had hipcc sink each load into
+    // its store's branch after the MFMAs — a global round trip per slot and tap
+    static_assert(PER <= 4, "posconv: at most four float4 slots per thread");
+    float4 b0, b1, b2, b3;
+    auto bload = [&](int j) {
+        const float4* src = wg + (int64_t)j * NB4;
+        const int t = (int)threadIdx.x;
+        b0 = src[min(t, NB4 - 1)];
+        if constexpr (PER > 1) b1 = src[min(t + 256, NB4 - 1)];
+        if constexpr (PER > 2) b2 = src[min(t + 512, NB4 - 1)];
+        if constexpr (PER > 3) b3 = src[min(t + 768, NB4 - 1)];
+    };
+    auto bstore = [&](int buf) {
+        float4* dst = reinterpret_cast<float4*>(wb[buf]);
+        const int t = (int)threadIdx.x;
+        if (t < NB4) dst[t] = b0;
+        if constexpr (PER > 1) if (t + 256 < NB4) dst[t + 256] = b1;
+        if constexpr (PER > 2) if (t + 512 < NB4) dst[t + 512] = b2;
+        if constexpr (PER > 3) if (t + 768 < NB4) dst[t + 768] = b3;
+    };
+    bload(0);
+    bstore(0);
     __syncthreads();
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
     f32x4 acc[2][NOB];
@@ -684,9 +699,8 @@ __global__ __launch_bounds__(256) void posconv_kernel(PosConvArgs a) {
     // A fragment rows: frame wv 32 + 16 fb + r16 of the tile, shifted by the tap
     const float* xrow = xa + (wv * 32 + r16) * RS + 4 * q;
     for (int j = 0; j < kPcK; ++j) {
-        if (j + 1 < kPcK) {
-            WX_PC_BLOAD(j + 1)
-        }
+        if (j + 1 < kPcK) bload(j + 1);
+        __builtin_amdgcn_sched_barrier(0);
         const float* bb = wb[j & 1] + (q * CG + r16) * 4;
 #pragma unroll
         for (int ic = 0; ic < NIC; ++ic) {
@@ -705,13 +719,9 @@ __global__ __launch_bounds__(256) void posconv_kernel(PosConvArgs a) {
                     acc[fb][ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[fb].w, bv[ob].w, acc[fb][ob], 0, 0, 0);
                 }
         }
-        if (j + 1 < kPcK) {
-            WX_PC_BSTORE((j + 1) & 1)
-        }
+        if (j + 1 < kPcK) bstore((j + 1) & 1);
         __syncthreads();
     }
-#undef WX_PC_BLOAD
-#undef WX_PC_BSTORE
     // accumulator (fb, ob) register v: frame 16 fb + 4 q + v of the wave's 32, output 16 ob + r16
 #pragma unroll
     for (int fb = 0; fb < 2; ++fb)

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
 // outputs (60 used) on v_mfma_f32_16x16x4_f32; + bias, written once.  fp32 (fma chains: not
 // bit-identical to the GEMM route, tests compare at fp32 tolerance).
 constexpr int kCkFrames = 128;
+
 // One weight slab in LDS (round 6): a block is 64 KB (Cin 80), so two blocks share a CU and
 // one's slab load and barriers hide under the other's MFMAs.  (Round 5 double-buffered the slab
 // — 84 KB, one block per CU, the next tap's store overlapped inside the block: 1 ms per hour
@@ -160,14 +161,28 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
         *reinterpret_cast<float4*>(xa + r * RS + 4 * c4) = v;
     }
     const float4* wg = reinterpret_cast<const float4*>(wp);
-    float4 breg[PER];
-#define WX_CT_BLOAD(j) \
-    _Pragma("unroll") for (int p = 0; p < PER; ++p) breg[p] = wg[(int64_t)(j) * NB4 + min((int)threadIdx.x + 256 * p, NB4 - 1)];
-#define WX_CT_BSTORE()                                                                    \
-    _Pragma("unroll") for (int p = 0; p < PER; ++p) if ((int)threadIdx.x + 256 * p < NB4) \
-        reinterpret_cast<float4*>(wb)[threadIdx.x + 256 * p] = breg[p];
-    WX_CT_BLOAD(0)
-    WX_CT_BSTORE()
+    // the next tap's slab in five named registers (a float4 array here stayed a stack object in
+    // scratch memory: each tap stored it there and loaded it back after the barrier)
+    static_assert(NB4 % 256 == 0 && PER <= 5, "conv_taps: whole float4 rows per thread");
+    float4 b0, b1, b2, b3, b4;
+    auto bload = [&](int j) {
+        const float4* src = wg + (int64_t)j * NB4 + threadIdx.x;
+        b0 = src[0];
+        b1 = src[256];
+        b2 = src[512];
+        b3 = src[768];
+        if constexpr (PER > 4) b4 = src[1024];
+    };
+    auto bstore = [&]() {
+        float4* dst = reinterpret_cast<float4*>(wb) + threadIdx.x;
+        dst[0] = b0;
+        dst[256] = b1;
+        dst[512] = b2;
+        dst[768] = b3;
+        if constexpr (PER > 4) dst[1024] = b4;
+    };
+    bload(0);
+    bstore();
     __syncthreads();
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6, q = l >> 4, r16 = l & 15;
     f32x4 acc[2][NOB];
@@ -178,9 +193,10 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
     const float* xrow = xa + (wv * 32 + r16) * RS + 4 * q;
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
-        if (j + 1 < KT) {
-            WX_CT_BLOAD(j + 1)
-        }
+        if (j + 1 < KT) bload(j + 1);
+        // (issued here, under the tap's MFMAs: hipcc otherwise sinks the loads to the store
+        // after the barrier, a global round trip per tap)
+        __builtin_amdgcn_sched_barrier(0);
         const float* bb = wb + (q * 64 + r16) * 4;
 #pragma unroll
         for (int ic = 0; ic < NIC; ++ic) {
@@ -201,12 +217,10 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
         }
         __syncthreads();  // every wave is done with tap j's slab
         if (j + 1 < KT) {
-            WX_CT_BSTORE()
+            bstore();
             __syncthreads();
         }
     }
-#undef WX_CT_BLOAD
-#undef WX_CT_BSTORE
     float* yb = y + (int64_t)b * Lout * Cout;
 #pragma unroll
     for (int fb = 0; fb < 2; ++fb)
