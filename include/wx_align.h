@@ -310,6 +310,16 @@ int wx_sincnet_stage_ex(const float* x, int64_t B, int64_t L, int32_t C, int64_t
  * where chunk c's first frame lands (non-decreasing).  out[f] = (sum over covering chunks, in
  * chunk order, of max_k scores[c, f - start_frame[c], k]) / (number of them), NaN outputs
  * masked out; `missing` where no chunk covers f.  Feeds wx_binarize on the device. */
+/* VAD producer (vad.py:198-240 -> pyannote SincNet's stage 1 on the shared-sinc route): the
+ * bias-free strided filterbank convolution (K taps) of one waveform span x [n] (fp32):
+ * y[t][c] = sum_{j < K} x[stride t + j] w_padded[j][c] for t < (n - K) / stride + 1, y
+ * time-major [rows][C].  w_padded [KP][C]: the K taps zero-padded to KP (a multiple of 4), so
+ * the kernel sums KP taps, reading zeros past the end of x.  Instantiated for pyannote's
+ * C = 80, KP = 260 (K = 251), stride <= 16.  fp32 (f32 MFMA: tolerance-equal to the unfold
+ * GEMM it replaces). */
+int wx_sinc_filterbank(const float* x, int64_t n, int32_t stride, const float* w_padded, int32_t C, int32_t K,
+                       int32_t KP, float* y, void* stream);
+
 /* VAD producer (vad.py:198-240 -> pyannote SincNet's stages 2 and 3): Conv1d(Cin, Cout, K)
  * with no padding and stride 1 over every window of a time-major batch x [B][L][Cin]
  * (contiguous, 16-byte aligned, Cin % 4 == 0, Cin <= 80, Cout <= 64, K == 5):

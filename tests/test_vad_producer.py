@@ -172,6 +172,27 @@ def test_shared_sinc_filterbank_matches_per_window(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [251, 252, 261, 2551, 80000 + 7, 16000 * 75 + 1234])
+def test_sinc_filterbank_kernel_vs_fp64_conv(n):
+    """wx_sinc_filterbank (the shared-sinc route's stage-1 convolution: 80 filters of 251 taps,
+    stride 10, taps zero-padded to 260, rows read in place) against an fp64 F.conv1d of the
+    same span, fp32 tolerance; spans that end inside a block of 256 rows, in the padded taps,
+    and a single row."""
+    import torch.nn.functional as F
+
+    from whisperx_amd import _lib
+
+    g = torch.Generator().manual_seed(n)
+    x = (torch.randn(n, generator=g) * 0.1).cuda()
+    w = (torch.randn(80, 251, generator=g) * 0.05).cuda()
+    wp = F.pad(w, (0, 9)).t().contiguous()
+    got = _lib.sinc_filterbank(x, wp, 251, 10)
+    ref = F.conv1d(x.double()[None, None], w.double()[:, None], stride=10)[0].t()
+    assert got.shape == ref.shape == ((n - 251) // 10 + 1, 80)
+    torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
 def test_sincnet_fused_epilogue_matches_torch_ops(monkeypatch):
     """PyanNet's forward with the fused SincNet epilogues against the same forward through
     torch's ops (WX_NO_SINC_EPILOGUE=1), both on the GEMM route: scores within float noise, and

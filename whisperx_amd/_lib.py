@@ -85,6 +85,7 @@ SIGNATURES = {
     "wx_vad_aggregate": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i64, _f32, _vp, _vp]),
     "wx_attention_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _f32, _vp]),
     "wx_conv1d_taps_tm": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
+    "wx_sinc_filterbank": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "wx_lstm_bidir_layer": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     "wx_posconv_packed": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _vp, _vp]),
     "wx_attention_f32_packed": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp,
@@ -591,6 +592,24 @@ def conv1d_taps_tm(x_tm: torch.Tensor, w_packed: torch.Tensor, bias, cout: int, 
     with torch.cuda.device(x_tm.device):
         _check(lib.wx_conv1d_taps_tm(_ptr(x_tm), B, L, C, _ptr(w_packed), _ptr(bias) if bias is not None else None,
                                      int(cout), int(k), _ptr(y), _stream(x_tm.device)))
+    return y
+
+
+def sinc_filterbank(x: torch.Tensor, w_padded: torch.Tensor, k: int, stride: int) -> torch.Tensor:
+    """wx_sinc_filterbank: the strided k-tap filterbank convolution of one contiguous fp32
+    waveform span x [n] with the taps zero-padded to w_padded [KP, C]; returns
+    [(n - k) // stride + 1, C] time-major."""
+    lib = load()
+    KP, C = (int(v) for v in w_padded.shape)
+    n = int(x.shape[0])
+    if x.dim() != 1 or not x.is_contiguous() or x.dtype != torch.float32 or not w_padded.is_contiguous() \
+            or w_padded.dtype != torch.float32 or not 0 < k <= KP:
+        raise WXError("sinc_filterbank: x must be a contiguous fp32 [n] span, w_padded a contiguous fp32 [KP >= k, C]")
+    F_out = (n - k) // stride + 1 if n >= k else 0
+    y = torch.empty((F_out, C), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device):
+        _check(lib.wx_sinc_filterbank(_ptr(x), n, int(stride), _ptr(w_padded), C, int(k), KP, _ptr(y),
+                                      _stream(x.device)))
     return y
 
 

@@ -51,27 +51,54 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
     const float* x = a.x + (int64_t)b * a.xb;
     float* y = a.y + (int64_t)b * a.Lp * a.C;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+    // (the window's input affine: a shared convolution with a per-window norm)
+    const float sc_in = a.in_scale ? a.in_scale[b] : 1.0f;
+    const float4 sh_in = a.in_scale ? reinterpret_cast<const float4*>(a.in_shift + (int64_t)b * a.C)[g]
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto pool = [&](float4 u, float4 v, float4 w) {
+        if (a.in_scale) {
+            u = make_float4(u.x * sc_in + sh_in.x, u.y * sc_in + sh_in.y, u.z * sc_in + sh_in.z, u.w * sc_in + sh_in.w);
+            v = make_float4(v.x * sc_in + sh_in.x, v.y * sc_in + sh_in.y, v.z * sc_in + sh_in.z, v.w * sc_in + sh_in.w);
+            w = make_float4(w.x * sc_in + sh_in.x, w.y * sc_in + sh_in.y, w.z * sc_in + sh_in.z, w.w * sc_in + sh_in.w);
+        }
+        if (a.do_abs) {
+            u = make_float4(fabsf(u.x), fabsf(u.y), fabsf(u.z), fabsf(u.w));
+            v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
+            w = make_float4(fabsf(w.x), fabsf(w.y), fabsf(w.z), fabsf(w.w));
+        }
+        return make_float4(nan_max(nan_max(u.x, v.x), w.x), nan_max(nan_max(u.y, v.y), w.y),
+                           nan_max(nan_max(u.z, v.z), w.z), nan_max(nan_max(u.w, v.w), w.w));
+    };
+    auto acc = [&](float4 p) {  // (rows of a thread in increasing order)
+        s0 += p.x; s1 += p.y; s2 += p.z; s3 += p.w;
+        q0 += (double)p.x * p.x; q1 += (double)p.y * p.y; q2 += (double)p.z * p.z; q3 += (double)p.w * p.w;
+    };
+    // four pooled rows per thread and pass: twelve 16-byte loads in flight instead of three (a
+    // latency-bound 3.7 TB/s before)
+    constexpr int kU = 4;
+    int t = r;
     if (active) {
-        for (int t = r; t < a.Lp; t += R) {
+        for (; t + (kU - 1) * R < a.Lp; t += kU * R) {
+            float4 u[kU], v[kU], w[kU];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                const float4* src = reinterpret_cast<const float4*>(x + (int64_t)3 * (t + k * R) * a.C) + g;
+                u[k] = src[0];
+                v[k] = src[G];
+                w[k] = src[2 * G];
+            }
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                const float4 p = pool(u[k], v[k], w[k]);
+                reinterpret_cast<float4*>(y + (int64_t)(t + k * R) * a.C)[g] = p;
+                acc(p);
+            }
+        }
+        for (; t < a.Lp; t += R) {
             const float4* src = reinterpret_cast<const float4*>(x + (int64_t)3 * t * a.C) + g;
-            float4 u = src[0], v = src[G], w = src[2 * G];
-            if (a.in_scale) {  // the window's input affine (a shared convolution, per-window norm)
-                const float sc = a.in_scale[b];
-                const float4 sh = reinterpret_cast<const float4*>(a.in_shift + (int64_t)b * a.C)[g];
-                u = make_float4(u.x * sc + sh.x, u.y * sc + sh.y, u.z * sc + sh.z, u.w * sc + sh.w);
-                v = make_float4(v.x * sc + sh.x, v.y * sc + sh.y, v.z * sc + sh.z, v.w * sc + sh.w);
-                w = make_float4(w.x * sc + sh.x, w.y * sc + sh.y, w.z * sc + sh.z, w.w * sc + sh.w);
-            }
-            if (a.do_abs) {
-                u = make_float4(fabsf(u.x), fabsf(u.y), fabsf(u.z), fabsf(u.w));
-                v = make_float4(fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w));
-                w = make_float4(fabsf(w.x), fabsf(w.y), fabsf(w.z), fabsf(w.w));
-            }
-            const float4 p = make_float4(nan_max(nan_max(u.x, v.x), w.x), nan_max(nan_max(u.y, v.y), w.y),
-                                         nan_max(nan_max(u.z, v.z), w.z), nan_max(nan_max(u.w, v.w), w.w));
+            const float4 p = pool(src[0], src[G], src[2 * G]);
             reinterpret_cast<float4*>(y + (int64_t)t * a.C)[g] = p;
-            s0 += p.x; s1 += p.y; s2 += p.z; s3 += p.w;
-            q0 += (double)p.x * p.x; q1 += (double)p.y * p.y; q2 += (double)p.z * p.z; q3 += (double)p.w * p.w;
+            acc(p);
         }
     }
     __shared__ double red[kThreads / 4][8];  // (R <= kThreads / 4 when G >= 4)
@@ -112,11 +139,21 @@ __global__ __launch_bounds__(kThreads) void sinc_stage_kernel(SincArgs a) {
     const float4 sh = make_float4(coef[2][4 * g], coef[2][4 * g + 1], coef[2][4 * g + 2], coef[2][4 * g + 3]);
     const float sl = a.slope;
     auto lrelu = [sl](float v) { return v > 0.0f ? v : v * sl; };
-    for (int t = r; t < a.Lp; t += R) {
+    auto norm = [&](float4 p) {
+        return make_float4(lrelu((p.x - mu.x) * sc.x + sh.x), lrelu((p.y - mu.y) * sc.y + sh.y),
+                           lrelu((p.z - mu.z) * sc.z + sh.z), lrelu((p.w - mu.w) * sc.w + sh.w));
+    };
+    t = r;
+    for (; t + (kU - 1) * R < a.Lp; t += kU * R) {
+        float4 p[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) p[k] = reinterpret_cast<const float4*>(y + (int64_t)(t + k * R) * a.C)[g];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) reinterpret_cast<float4*>(y + (int64_t)(t + k * R) * a.C)[g] = norm(p[k]);
+    }
+    for (; t < a.Lp; t += R) {
         float4* d = reinterpret_cast<float4*>(y + (int64_t)t * a.C) + g;
-        const float4 p = *d;
-        *d = make_float4(lrelu((p.x - mu.x) * sc.x + sh.x), lrelu((p.y - mu.y) * sc.y + sh.y),
-                         lrelu((p.z - mu.z) * sc.z + sh.z), lrelu((p.w - mu.w) * sc.w + sh.w));
+        *d = norm(*d);
     }
 }
 
@@ -234,6 +271,58 @@ __global__ __launch_bounds__(256) void conv_taps_kernel(const float* __restrict_
                 if (c < Cout) yb[(int64_t)t * Cout + c] = acc[fb][ob][v] + (bias ? bias[c] : 0.f);
             }
         }
+}
+
+// ------------------------------------------------------------------------------------
+// SincNet's filterbank over a waveform span (the shared-sinc route: pyannote SincNet stage 1,
+// a bias-free Conv1d(1, C, k = 251, stride 10), run once per batch of overlapping windows):
+// y[t][c] = sum_{j < KP} x[S t + j] w[j][c], KP = k zero-padded to a multiple of 4 (zeros past
+// the end of x), t < (n - k) / S + 1.  As a
+// GEMM on the unfold view (rows overlap: stride S < KP) torch first copied every patch row
+// out (~1 GB chunks, 1.7 ms per hour of audio) and then multiplied (3.0 ms).  Here the rows
+// are read where they lie: a block stages the 256 S + KP samples of its 256 output rows in
+// LDS once; wave w owns channels 16 w .. 16 w + 15 and keeps their KP x 16 filter taps as
+// v_mfma_f32_16x16x4_f32 B fragments in registers for the whole block; each MFMA's A fragment
+// (16 rows x 4 taps) is one LDS read per lane at S (row) + tap.  fp32 (tolerance-equal to
+// the GEMM: a different summation order).
+constexpr int kSfRows = 256;   // output rows per block
+constexpr int kSfMaxS = 16;    // stride bound of the LDS window
+
+template <int NT, int KP>  // NT 16-channel tiles (C = 16 NT), KP padded taps
+__global__ __launch_bounds__(64 * NT) void sinc_fb_kernel(const float* __restrict__ x, int64_t n, int S,
+                                                          const float* __restrict__ w /* [KP][16 NT] */,
+                                                          float* __restrict__ y, int64_t F) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    constexpr int C = 16 * NT, NS = KP / 4;
+    static_assert(KP % 4 == 0, "taps padded to a multiple of 4");
+    __shared__ float xs[kSfRows * kSfMaxS + KP];
+    const int64_t t0 = (int64_t)blockIdx.x * kSfRows;
+    const int64_t s0 = t0 * S;
+    const int nw = kSfRows * S + KP;
+    for (int i = (int)threadIdx.x; i < nw; i += 64 * NT) xs[i] = s0 + i < n ? x[s0 + i] : 0.f;
+    const int l = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6, r16 = l & 15, kq = l >> 4;
+    float b[NS];  // B[k = kq][col = r16] of tap group s: w[4 s + kq][16 wv + r16]
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[s] = w[(4 * s + kq) * C + 16 * wv + r16];
+    __syncthreads();
+    // two row tiles at a time (two independent accumulator chains)
+    for (int rt = 0; rt < kSfRows / 16; rt += 2) {
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        const float* x0 = xs + S * (16 * rt + r16) + kq;
+        const float* x1 = x0 + 16 * S;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[4 * s], b[s], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[4 * s], b[s], a1, 0, 0, 0);
+        }
+        // D[row 4 kq + v][col r16]
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int64_t t = t0 + 16 * rt + 4 * kq + v;
+            if (t < F) y[t * C + 16 * wv + r16] = a0[v];
+            if (t + 16 < F) y[(t + 16) * C + 16 * wv + r16] = a1[v];
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -392,6 +481,23 @@ extern "C" int wx_lstm_bidir_layer(const float* xp, const float* whh, float* y, 
     const dim3 grid((unsigned)((B + kLR - 1) / kLR), 2);
     hipLaunchKernelGGL(lstm_layer_kernel, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xp, whh, y,
                        (int)B, (int)T);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WX_OK : (int)e;
+}
+
+extern "C" int wx_sinc_filterbank(const float* x, int64_t n, int32_t stride, const float* w_padded, int32_t C,
+                                  int32_t K, int32_t KP, float* y, void* stream) {
+    using namespace wxv;
+    if (n < 0 || stride <= 0 || stride > kSfMaxS || K <= 0 || K > KP || !x || !w_padded || !y) return WX_E_INVALID;
+    if (n < K) return WX_OK;  // no output row
+    const int64_t F = (n - K) / stride + 1;
+    if ((F + kSfRows - 1) / kSfRows > 0x7fffffff) return WX_E_INVALID;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)((F + kSfRows - 1) / kSfRows));
+    if (C == 80 && KP == 260)
+        hipLaunchKernelGGL((sinc_fb_kernel<5, 260>), grid, dim3(64 * 5), 0, s, x, n, (int)stride, w_padded, y, F);
+    else
+        return WX_E_INVALID;
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? WX_OK : (int)e;
 }

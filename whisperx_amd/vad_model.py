@@ -267,8 +267,14 @@ def _conv_global(x: torch.Tensor, w: torch.Tensor, stride: int) -> torch.Tensor:
     n = x.shape[0]
     F_out = (n - k) // stride + 1
     kp = -(-k // stride) * stride
-    xs = F.pad(x, (0, kp - k)) if kp > k else x
     wp = F.pad(w, (0, kp - k)).t().contiguous()  # [kp, C]
+    if (x.is_cuda and C == 80 and kp == 260 and stride <= 16 and x.dtype == torch.float32
+            and not os.environ.get("WX_NO_SINC_KERNEL")):
+        # wx_sinc_filterbank: the rows read where they lie (no patch copy)
+        from . import _lib
+
+        return _lib.sinc_filterbank(x.contiguous(), wp, k, stride)
+    xs = F.pad(x, (0, kp - k)) if kp > k else x
     pat = xs.unfold(0, kp, stride)[:F_out]  # [F, kp] view
     out = torch.empty((F_out, C), dtype=x.dtype, device=x.device)
     rows = max(1, _PATCH_BYTES // (kp * x.element_size()))
