@@ -52,7 +52,7 @@ def classify(n):
         return "lstm_recurrence"
     if "vad_aggregate" in n:
         return "overlap_add"
-    if n.startswith("Cijk_Ailk"):
+    if "sinc_fb_kernel" in n or n.startswith("Cijk_Ailk"):  # (wx_sinc_filterbank; before it the unfold GEMM)
         return "sinc_filterbank_gemm"
     if "MT256x256" in n:
         return "lstm_input_gemms"
