@@ -248,12 +248,25 @@ __device__ __forceinline__ void conv0_samples(const float* __restrict__ x, int64
     }
 }
 
+// A wave whose kC0R rows read only samples inside the waveform (all but the last) reads them
+// straight from memory at wave-uniform addresses: scalar loads into SGPRs that the FMAs take as
+// operands — no v_readlane per tap and none of the SGPR-hazard s_nops after it (the register
+// form, conv0_samples + conv0_row, stays for the last wave).  Same fma chain per row.
+template <int K, int S>
+__device__ __forceinline__ float conv0_row_s(const float* __restrict__ xs /* wave-uniform */, int r,
+                                             const float (&w)[K], float b) {
+    float acc = b;
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc = fmaf(xs[r * S + j], w[j], acc);
+    return acc;
+}
+
 template <int K, int S>
 __global__ __launch_bounds__(256) void conv0_stats_rl_kernel(const float* __restrict__ x, int64_t nsamp, int64_t L,
                                                              const float* __restrict__ wt,
                                                              const float* __restrict__ bias, int C,
                                                              double* __restrict__ part /* [nblk][2][C] */) {
-    const int lc = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lc = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int c = blockIdx.x * 64 + lc;
     const int cc = min(c, C - 1);
     float w[K];
@@ -261,16 +274,28 @@ __global__ __launch_bounds__(256) void conv0_stats_rl_kernel(const float* __rest
     for (int j = 0; j < K; ++j) w[j] = wt[(int64_t)cc * K + j];
     const float b = bias ? bias[cc] : 0.f;
     const int64_t t0 = ((int64_t)blockIdx.y * 4 + wv) * kC0R;
-    float sv[((kC0R - 1) * S + K + 63) / 64];
-    conv0_samples<K, S>(x, nsamp, t0, sv);
     const int64_t nr = L - t0;
     double sm = 0.0, q = 0.0;
+    if (t0 * S + (kC0R - 1) * S + K <= nsamp) {
+        const float* xs = x + t0 * S;
 #pragma unroll
-    for (int r = 0; r < kC0R; ++r) {
-        const double d = (double)conv0_row<K, S>(sv, r, w, b);
-        if (r < nr) {
-            sm += d;
-            q = fma(d, d, q);
+        for (int r = 0; r < kC0R; ++r) {
+            const double d = (double)conv0_row_s<K, S>(xs, r, w, b);
+            if (r < nr) {
+                sm += d;
+                q = fma(d, d, q);
+            }
+        }
+    } else {
+        float sv[((kC0R - 1) * S + K + 63) / 64];
+        conv0_samples<K, S>(x, nsamp, t0, sv);
+#pragma unroll
+        for (int r = 0; r < kC0R; ++r) {
+            const double d = (double)conv0_row<K, S>(sv, r, w, b);
+            if (r < nr) {
+                sm += d;
+                q = fma(d, d, q);
+            }
         }
     }
     __shared__ double ss[4][64], qq[4][64];
@@ -291,7 +316,7 @@ __global__ __launch_bounds__(256) void conv0_apply_rl_kernel(const float* __rest
                                                              const float* __restrict__ bias, int C,
                                                              const float* __restrict__ ab, int gelu,
                                                              float* __restrict__ y) {
-    const int lc = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lc = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int c = blockIdx.x * 64 + lc;
     const int cc = min(c, C - 1);
     float w[K];
@@ -300,14 +325,25 @@ __global__ __launch_bounds__(256) void conv0_apply_rl_kernel(const float* __rest
     const float b = bias ? bias[cc] : 0.f;
     const float sa = ab[cc], sb = ab[C + cc];
     const int64_t t0 = ((int64_t)blockIdx.y * 4 + wv) * kC0R;
-    float sv[((kC0R - 1) * S + K + 63) / 64];
-    conv0_samples<K, S>(x, nsamp, t0, sv);
     const int64_t nr = L - t0;
+    float* yr = y + t0 * C + c;  // (row r at yr + r C)
+    if (t0 * S + (kC0R - 1) * S + K <= nsamp) {
+        const float* xs = x + t0 * S;
 #pragma unroll
-    for (int r = 0; r < kC0R; ++r) {
-        float v = conv0_row<K, S>(sv, r, w, b) * sa + sb;
-        if (gelu) v = gelu_erf0(v);
-        if (r < nr && c < C) y[(t0 + r) * C + c] = v;
+        for (int r = 0; r < kC0R; ++r) {
+            float v = conv0_row_s<K, S>(xs, r, w, b) * sa + sb;
+            if (gelu) v = gelu_erf0(v);
+            if (r < nr && c < C) yr[(int64_t)r * C] = v;
+        }
+    } else {
+        float sv[((kC0R - 1) * S + K + 63) / 64];
+        conv0_samples<K, S>(x, nsamp, t0, sv);
+#pragma unroll
+        for (int r = 0; r < kC0R; ++r) {
+            float v = conv0_row<K, S>(sv, r, w, b) * sa + sb;
+            if (gelu) v = gelu_erf0(v);
+            if (r < nr && c < C) yr[(int64_t)r * C] = v;
+        }
     }
 }
 
